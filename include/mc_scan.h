@@ -1,0 +1,139 @@
+/*
+ * mc_scan.h -- C ABI of the MI355X selective-scan kernels (libmamba_clip_amd.so).
+ *
+ * Replaces the native boundary the reference reaches through
+ *   mamba_ssm.ops.selective_scan_interface.selective_scan_fn
+ *     -> SelectiveScanFn.forward/backward -> selective_scan_cuda.fwd/bwd
+ * (third-party, not vendored; imported at /root/reference/src/mamba_clip/model.py:27-28,
+ *  called at model.py:539-550; reference semantics embedded at model.py:83-169).
+ *
+ *   mc_scan_fwd  <- selective_scan_cuda.fwd(u, delta, A, B, C, D, z, delta_bias, softplus)
+ *   mc_scan_bwd  <- selective_scan_cuda.bwd(u, delta, A, B, C, D, z, delta_bias, dout,
+ *                                           x_chunks, out, dz, softplus, recompute_out_z)
+ *
+ * Contract
+ *   - Plain pointers and sizes only.  Every device buffer (inputs, outputs,
+ *     chunk states, workspace) is allocated by the caller; the library never
+ *     allocates, frees or synchronises.
+ *   - Launches are asynchronous on the given stream (hipStream_t passed as void*).
+ *   - Returns MC_OK (0) or a negative code; mc_last_error() gives a
+ *     thread-local message (the Python layer raises RuntimeError with it, as
+ *     the upstream TORCH_CHECKs do).
+ *   - Re-entrant; no global mutable state.
+ *   - Layout: u/delta/z/out/dout/du/ddelta/dz are (batch, dim, seqlen) with unit
+ *     stride along seqlen; B/C (and dB/dC) are (batch, n_groups, dstate, seqlen)
+ *     with unit stride along seqlen; A (dim, dstate) fp32; D, delta_bias
+ *     (dim,) fp32.  Channel d reads group d / (dim / n_groups).
+ */
+#ifndef MAMBA_CLIP_AMD_MC_SCAN_H
+#define MAMBA_CLIP_AMD_MC_SCAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum mc_dtype {
+  MC_DTYPE_F32 = 0,
+  MC_DTYPE_BF16 = 1,
+  MC_DTYPE_F16 = 2
+} mc_dtype;
+
+enum {
+  MC_OK = 0,
+  MC_ERR_INVALID = -1,   /* null pointer / bad argument */
+  MC_ERR_DTYPE = -2,     /* unsupported dtype combination */
+  MC_ERR_SHAPE = -3,     /* bad shape (dim % n_groups, dstate > MC_SCAN_MAX_DSTATE, ...) */
+  MC_ERR_LAUNCH = -4,    /* kernel launch failed */
+  MC_ERR_WORKSPACE = -5  /* workspace too small */
+};
+
+#define MC_SCAN_MAX_DSTATE 32
+/* sequence positions per chunk; chunk states are saved once per chunk */
+#define MC_SCAN_CHUNK 32
+
+typedef struct mc_scan_fwd_params {
+  int32_t batch, dim, seqlen, dstate, n_groups;
+  int32_t itype;            /* mc_dtype of u, delta, z, out */
+  int32_t wtype;            /* mc_dtype of B, C */
+  int32_t delta_softplus;   /* apply softplus(delta + delta_bias) */
+  /* element strides (seqlen stride is 1 everywhere) */
+  int64_t u_batch_stride, u_dim_stride;
+  int64_t delta_batch_stride, delta_dim_stride;
+  int64_t z_batch_stride, z_dim_stride;
+  int64_t out_batch_stride, out_dim_stride;
+  int64_t B_batch_stride, B_group_stride, B_dstate_stride;
+  int64_t C_batch_stride, C_group_stride, C_dstate_stride;
+  const void* u;
+  const void* delta;
+  const float* A;           /* (dim, dstate) contiguous */
+  const void* B;
+  const void* C;
+  const float* D;           /* nullable, (dim,) */
+  const void* z;            /* nullable: out = (y + D u) * silu(z) */
+  const float* delta_bias;  /* nullable, (dim,) */
+  void* out;
+  float* chunk_states;      /* nullable: (batch, dim, n_chunks, dstate) fp32, state at END of each chunk */
+  float* last_state;        /* nullable: (batch, dim, dstate) fp32 */
+} mc_scan_fwd_params;
+
+typedef struct mc_scan_bwd_params {
+  int32_t batch, dim, seqlen, dstate, n_groups;
+  int32_t itype, wtype, delta_softplus;
+  /* inputs, same layout rules as forward (seqlen stride 1) */
+  int64_t u_batch_stride, u_dim_stride;
+  int64_t delta_batch_stride, delta_dim_stride;
+  int64_t z_batch_stride, z_dim_stride;
+  int64_t dout_batch_stride, dout_dim_stride;
+  int64_t B_batch_stride, B_group_stride, B_dstate_stride;
+  int64_t C_batch_stride, C_group_stride, C_dstate_stride;
+  const void* u;
+  const void* delta;
+  const float* A;
+  const void* B;
+  const void* C;
+  const float* D;             /* nullable */
+  const void* z;              /* nullable */
+  const float* delta_bias;    /* nullable */
+  const void* dout;           /* gradient of out (itype) */
+  const float* chunk_states;  /* REQUIRED: produced by mc_scan_fwd on the same inputs */
+  /* outputs: du/ddelta/dz contiguous (batch, dim, seqlen) in itype; dB/dC
+   * contiguous (batch, n_groups, dstate, seqlen) in wtype; dA (dim, dstate),
+   * dD (dim,), ddelta_bias (dim,) fp32.  dz / dD / ddelta_bias nullable when
+   * the corresponding input is absent. */
+  void* du;
+  void* ddelta;
+  void* dz;
+  void* dB;
+  void* dC;
+  float* dA;
+  float* dD;
+  float* ddelta_bias;
+  void* workspace;            /* >= mc_scan_bwd_workspace_bytes(...) bytes, 256-B aligned */
+  size_t workspace_bytes;
+} mc_scan_bwd_params;
+
+/* number of MC_SCAN_CHUNK-long chunks covering seqlen */
+int32_t mc_scan_n_chunks(int32_t seqlen);
+
+/* bytes of fp32 chunk states the forward writes for a training call */
+size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate);
+
+/* workspace the backward needs (partial-sum slabs; deterministic reductions) */
+size_t mc_scan_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate,
+                                   int32_t n_groups);
+
+int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream);
+int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream);
+
+/* thread-local text of the last error returned on this thread */
+const char* mc_last_error(void);
+/* library version string */
+const char* mc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAMBA_CLIP_AMD_MC_SCAN_H */

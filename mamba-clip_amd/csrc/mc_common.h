@@ -1,0 +1,142 @@
+// mc_common.h -- shared device/host helpers for the MI355X (gfx950) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string>
+
+namespace mc {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// ---------------------------------------------------------------- dtypes
+// Element types as they sit in HBM.  bf16 and f16 travel as raw 16-bit words
+// and are widened in registers; all arithmetic is fp32.
+using bf16_t = __bf16;
+using f16_t = _Float16;
+
+template <typename T> struct ElemTraits;
+template <> struct ElemTraits<float> { static constexpr int kVec = 4; };   // 16 B = 4 elems
+template <> struct ElemTraits<bf16_t> { static constexpr int kVec = 8; };  // 16 B = 8 elems
+template <> struct ElemTraits<f16_t> { static constexpr int kVec = 8; };
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16_t x) { return (float)x; }
+__device__ __forceinline__ float to_f(f16_t x) { return (float)x; }
+
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float x) { return (bf16_t)x; }  // RNE, v_cvt_pk_bf16_f32
+template <> __device__ __forceinline__ f16_t from_f<f16_t>(float x) { return (f16_t)x; }
+
+// ---------------------------------------------------------------- 16-byte vectors
+// A 16-B vector of 4 (fp32) or 8 (16-bit) elements lives in a uint4; element
+// access uses compile-time indices only (no addressable arrays, so nothing is
+// demoted to scratch).
+__device__ __forceinline__ uint32_t word_of(const uint4& q, int i) {
+  return i == 0 ? q.x : (i == 1 ? q.y : (i == 2 ? q.z : q.w));
+}
+
+template <typename T> __device__ __forceinline__ float elem_f(const uint4& q, int i);
+template <> __device__ __forceinline__ float elem_f<float>(const uint4& q, int i) {
+  return __uint_as_float(word_of(q, i));
+}
+template <> __device__ __forceinline__ float elem_f<bf16_t>(const uint4& q, int i) {
+  const uint32_t w = word_of(q, i >> 1);
+  return __uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16));
+}
+template <> __device__ __forceinline__ float elem_f<f16_t>(const uint4& q, int i) {
+  const uint32_t w = word_of(q, i >> 1);
+  return (float)__builtin_bit_cast(f16_t, (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu)));
+}
+
+template <typename T> __device__ __forceinline__ uint32_t bits16(float x) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, from_f<T>(x));
+}
+// pack kVec fp32 values into the element type
+template <typename T> __device__ __forceinline__ uint4 pack_f(const float (&v)[ElemTraits<T>::kVec]);
+template <> __device__ __forceinline__ uint4 pack_f<float>(const float (&v)[4]) {
+  return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+}
+template <typename T>
+__device__ __forceinline__ uint4 pack16_impl(const float (&v)[8]) {
+  return make_uint4(bits16<T>(v[0]) | (bits16<T>(v[1]) << 16), bits16<T>(v[2]) | (bits16<T>(v[3]) << 16),
+                    bits16<T>(v[4]) | (bits16<T>(v[5]) << 16), bits16<T>(v[6]) | (bits16<T>(v[7]) << 16));
+}
+template <> __device__ __forceinline__ uint4 pack_f<bf16_t>(const float (&v)[8]) { return pack16_impl<bf16_t>(v); }
+template <> __device__ __forceinline__ uint4 pack_f<f16_t>(const float (&v)[8]) { return pack16_impl<f16_t>(v); }
+
+// raw 16-bit/32-bit element bits
+template <typename T> __device__ __forceinline__ uint32_t ld_bits(const T* p) {
+  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const uint32_t*>(p);
+  else return (uint32_t)*reinterpret_cast<const uint16_t*>(p);
+}
+template <typename T> __device__ __forceinline__ void st_bits(T* p, uint32_t b) {
+  if constexpr (sizeof(T) == 4) *reinterpret_cast<uint32_t*>(p) = b;
+  else *reinterpret_cast<uint16_t*>(p) = (uint16_t)b;
+}
+
+// Vector load of elements [0, nvalid) from p, zero-filled above; nvalid in [0, kVec].
+template <typename T>
+__device__ __forceinline__ uint4 ld16_masked(const T* __restrict__ p, int nvalid) {
+  constexpr int N = ElemTraits<T>::kVec;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t b = (i < nvalid) ? ld_bits(p + i) : 0u;
+    if constexpr (sizeof(T) == 4) w[i] = b;
+    else w[i >> 1] |= b << (16 * (i & 1));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <typename T>
+__device__ __forceinline__ void st16_masked(T* __restrict__ p, const uint4& q, int nvalid) {
+  constexpr int N = ElemTraits<T>::kVec;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i < nvalid) {
+      if constexpr (sizeof(T) == 4) st_bits(p + i, word_of(q, i));
+      else st_bits(p + i, (word_of(q, i >> 1) >> (16 * (i & 1))) & 0xffffu);
+    }
+  }
+}
+__device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void st16(void* p, const uint4& q) { *reinterpret_cast<uint4*>(p) = q; }
+
+// exp2 on the transcendental unit (v_exp_f32)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// softplus with torch's threshold (F.softplus: x > 20 -> x).  Branch-free
+// (selects only) so it does not split the recurrence's basic block.
+__device__ __forceinline__ float softplus_f(float x) {
+  const float t = fast_exp2(fminf(x, 20.f) * kLog2e);
+  const float lg = fast_log2(1.f + t) * kLn2;
+  const float series = t * (1.f - 0.5f * t);  // log1p(t) for tiny t (softplus(-30) != 0)
+  const float r = t < 1e-4f ? series : lg;
+  return x > 20.f ? x : r;
+}
+// d softplus / dx = sigmoid(x)
+__device__ __forceinline__ float sigmoid_f(float x) { return fast_rcp(1.f + fast_exp2(-x * kLog2e)); }
+
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
+
+// ---------------------------------------------------------------- host error plumbing
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+#define MC_CHECK(cond, code, ...)      \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::mc::set_error(__VA_ARGS__);    \
+      return (code);                   \
+    }                                  \
+  } while (0)
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace mc

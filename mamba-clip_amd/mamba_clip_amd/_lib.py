@@ -1,0 +1,109 @@
+"""ctypes binding of libmamba_clip_amd.so (the C ABI declared in include/*.h).
+
+The product path has NO fallback: if the HIP library is missing or fails to
+load, importing any op raises.  Build it with
+``make -C mamba-clip_amd`` (or ``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmamba_clip_amd.so")
+
+MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16 = 0, 1, 2
+MC_SCAN_CHUNK = 32
+MC_SCAN_MAX_DSTATE = 32
+
+c_i32, c_i64, c_vp, c_fp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p
+
+
+class ScanFwdParams(ctypes.Structure):
+    """Mirror of ``mc_scan_fwd_params`` (include/mc_scan.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("dim", c_i32), ("seqlen", c_i32), ("dstate", c_i32), ("n_groups", c_i32),
+        ("itype", c_i32), ("wtype", c_i32), ("delta_softplus", c_i32),
+        ("u_batch_stride", c_i64), ("u_dim_stride", c_i64),
+        ("delta_batch_stride", c_i64), ("delta_dim_stride", c_i64),
+        ("z_batch_stride", c_i64), ("z_dim_stride", c_i64),
+        ("out_batch_stride", c_i64), ("out_dim_stride", c_i64),
+        ("B_batch_stride", c_i64), ("B_group_stride", c_i64), ("B_dstate_stride", c_i64),
+        ("C_batch_stride", c_i64), ("C_group_stride", c_i64), ("C_dstate_stride", c_i64),
+        ("u", c_vp), ("delta", c_vp), ("A", c_fp), ("B", c_vp), ("C", c_vp),
+        ("D", c_fp), ("z", c_vp), ("delta_bias", c_fp),
+        ("out", c_vp), ("chunk_states", c_fp), ("last_state", c_fp),
+    ]
+
+
+class ScanBwdParams(ctypes.Structure):
+    """Mirror of ``mc_scan_bwd_params`` (include/mc_scan.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("dim", c_i32), ("seqlen", c_i32), ("dstate", c_i32), ("n_groups", c_i32),
+        ("itype", c_i32), ("wtype", c_i32), ("delta_softplus", c_i32),
+        ("u_batch_stride", c_i64), ("u_dim_stride", c_i64),
+        ("delta_batch_stride", c_i64), ("delta_dim_stride", c_i64),
+        ("z_batch_stride", c_i64), ("z_dim_stride", c_i64),
+        ("dout_batch_stride", c_i64), ("dout_dim_stride", c_i64),
+        ("B_batch_stride", c_i64), ("B_group_stride", c_i64), ("B_dstate_stride", c_i64),
+        ("C_batch_stride", c_i64), ("C_group_stride", c_i64), ("C_dstate_stride", c_i64),
+        ("u", c_vp), ("delta", c_vp), ("A", c_fp), ("B", c_vp), ("C", c_vp),
+        ("D", c_fp), ("z", c_vp), ("delta_bias", c_fp), ("dout", c_vp), ("chunk_states", c_fp),
+        ("du", c_vp), ("ddelta", c_vp), ("dz", c_vp), ("dB", c_vp), ("dC", c_vp),
+        ("dA", c_fp), ("dD", c_fp), ("ddelta_bias", c_fp),
+        ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+# symbol -> (restype, argtypes); every entry point include/*.h declares
+SYMBOLS = {
+    "mc_last_error": (ctypes.c_char_p, []),
+    "mc_version": (ctypes.c_char_p, []),
+    "mc_scan_n_chunks": (c_i32, [c_i32]),
+    "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
+    "mc_scan_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
+    "mc_scan_fwd": (ctypes.c_int, [ctypes.POINTER(ScanFwdParams), c_vp]),
+    "mc_scan_bwd": (ctypes.c_int, [ctypes.POINTER(ScanBwdParams), c_vp]),
+}
+
+_lib = None
+
+
+def load():
+    """Load the library (once).  Raises if it is absent -- no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"mamba_clip_amd: HIP library not found at {LIB_PATH}; build it with "
+            "`make -C mamba-clip_amd` (gfx950).  There is no CPU fallback.")
+    import torch  # noqa: F401  -- load torch's libamdhip64 first: one HIP runtime per process
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().mc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def dtype_code(dt):
+    import torch
+    codes = {torch.float32: MC_DTYPE_F32, torch.bfloat16: MC_DTYPE_BF16, torch.float16: MC_DTYPE_F16}
+    if dt not in codes:
+        raise RuntimeError(f"mamba_clip_amd: unsupported dtype {dt} (float32, bfloat16, float16 only)")
+    return codes[dt]
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None):
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

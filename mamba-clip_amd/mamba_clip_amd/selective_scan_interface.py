@@ -1,0 +1,178 @@
+"""``selective_scan_fn`` -- drop-in for mamba_ssm's op, backed by HIP kernels.
+
+Reference boundary: /root/reference/src/mamba_clip/model.py:27-28 imports
+``mamba_ssm.ops.selective_scan_interface.selective_scan_fn`` and calls it at
+model.py:539-550 (keyword style).  Same signature, same argument meaning, same
+outputs (``out`` or ``(out, last_state)``), autograd-capable, errors surface as
+``RuntimeError`` like upstream's TORCH_CHECKs.  Semantics: model.py:83-169.
+
+The forward runs ``mc_scan_fwd`` and, when a gradient will be needed, saves
+fp32 chunk states (one per MC_SCAN_CHUNK positions); the backward runs
+``mc_scan_bwd`` from them.  Both launch on the current HIP stream and never
+synchronise.  There is no CPU / eager fallback.
+"""
+import torch
+
+from . import _lib
+
+
+def _prep_bc(M, name):
+    """(B, N, L) -> (B, 1, N, L); (B, G, N, L) kept.  Unit stride along L."""
+    if M.dim() == 3:
+        M = M.unsqueeze(1)
+    elif M.dim() != 4:
+        raise RuntimeError(f"selective_scan_fn: {name} must be (B, N, L) or (B, G, N, L) (variable {name}); "
+                           f"constant (D, N) {name} is not supported")
+    if M.stride(-1) != 1:
+        M = M.contiguous()
+    return M
+
+
+def _last_dim_contig(x):
+    return x if x is None or x.stride(-1) == 1 else x.contiguous()
+
+
+def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
+    if not u.is_cuda:
+        raise RuntimeError("selective_scan_fn: inputs must be on the GPU (no CPU path)")
+    if A.is_complex():
+        raise RuntimeError("selective_scan_fn: complex A is not supported")
+    if delta.dtype != u.dtype or (z is not None and z.dtype != u.dtype):
+        raise RuntimeError("selective_scan_fn: u, delta and z must share a dtype")
+    if B.dtype not in (torch.float32, u.dtype) or C.dtype != B.dtype:
+        raise RuntimeError("selective_scan_fn: B/C must be float32 or the input dtype, and equal")
+    batch, dim, L = u.shape
+    if delta.shape != u.shape or (z is not None and z.shape != u.shape):
+        raise RuntimeError("selective_scan_fn: u, delta, z shape mismatch")
+    if A.shape[0] != dim:
+        raise RuntimeError("selective_scan_fn: A must be (D, N)")
+    dstate = A.shape[1]
+    if dstate > _lib.MC_SCAN_MAX_DSTATE:
+        raise RuntimeError(f"selective_scan_fn: dstate {dstate} > {_lib.MC_SCAN_MAX_DSTATE}")
+    for M in (B, C):
+        if M.shape[0] != batch or M.shape[2] != dstate or M.shape[3] != L:
+            raise RuntimeError("selective_scan_fn: B/C must be (B, G, N, L)")
+    if dim % B.shape[1] != 0:
+        raise RuntimeError("selective_scan_fn: dim must be divisible by n_groups")
+
+
+def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last):
+    """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None)."""
+    lib = _lib.load()
+    batch, dim, L = u.shape
+    dstate = A.shape[1]
+    G = B.shape[1]
+    out = torch.empty_like(u, memory_format=torch.contiguous_format)
+    nch = _lib.MC_SCAN_CHUNK and lib.mc_scan_n_chunks(L)
+    states = (torch.empty(batch, dim, nch, dstate, device=u.device, dtype=torch.float32)
+              if want_states else None)
+    last = (torch.empty(batch, dim, dstate, device=u.device, dtype=torch.float32)
+            if want_last and not want_states else None)
+    p = _lib.ScanFwdParams()
+    p.batch, p.dim, p.seqlen, p.dstate, p.n_groups = batch, dim, L, dstate, G
+    p.itype, p.wtype = _lib.dtype_code(u.dtype), _lib.dtype_code(B.dtype)
+    p.delta_softplus = int(bool(delta_softplus))
+    p.u_batch_stride, p.u_dim_stride = u.stride(0), u.stride(1)
+    p.delta_batch_stride, p.delta_dim_stride = delta.stride(0), delta.stride(1)
+    if z is not None:
+        p.z_batch_stride, p.z_dim_stride = z.stride(0), z.stride(1)
+    p.out_batch_stride, p.out_dim_stride = out.stride(0), out.stride(1)
+    p.B_batch_stride, p.B_group_stride, p.B_dstate_stride = B.stride(0), B.stride(1), B.stride(2)
+    p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
+    p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()
+    p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
+    p.out, p.chunk_states, p.last_state = out.data_ptr(), _lib.ptr(states), _lib.ptr(last)
+    _lib.check(lib.mc_scan_fwd(p, _lib.stream_handle(u.device)), "mc_scan_fwd")
+    if want_last and states is not None:
+        last = states[:, :, -1, :] if nch > 0 else torch.zeros(batch, dim, dstate, device=u.device)
+    return out, states, last
+
+
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
+    lib = _lib.load()
+    batch, dim, L = u.shape
+    dstate = A.shape[1]
+    G = B.shape[1]
+    dout = dout.contiguous()
+    du = torch.empty_like(u, memory_format=torch.contiguous_format)
+    ddelta = torch.empty_like(delta, memory_format=torch.contiguous_format)
+    dz = torch.empty_like(z, memory_format=torch.contiguous_format) if z is not None else None
+    dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
+    dC = torch.empty(C.shape, device=u.device, dtype=C.dtype)
+    dA = torch.empty(dim, dstate, device=u.device, dtype=torch.float32)
+    dD = torch.empty(dim, device=u.device, dtype=torch.float32) if D is not None else None
+    dbias = torch.empty(dim, device=u.device, dtype=torch.float32) if delta_bias is not None else None
+    ws_bytes = lib.mc_scan_bwd_workspace_bytes(batch, dim, L, dstate, G)
+    ws = torch.empty(max(ws_bytes, 1), device=u.device, dtype=torch.uint8)
+    p = _lib.ScanBwdParams()
+    p.batch, p.dim, p.seqlen, p.dstate, p.n_groups = batch, dim, L, dstate, G
+    p.itype, p.wtype = _lib.dtype_code(u.dtype), _lib.dtype_code(B.dtype)
+    p.delta_softplus = int(bool(delta_softplus))
+    p.u_batch_stride, p.u_dim_stride = u.stride(0), u.stride(1)
+    p.delta_batch_stride, p.delta_dim_stride = delta.stride(0), delta.stride(1)
+    if z is not None:
+        p.z_batch_stride, p.z_dim_stride = z.stride(0), z.stride(1)
+    p.dout_batch_stride, p.dout_dim_stride = dout.stride(0), dout.stride(1)
+    p.B_batch_stride, p.B_group_stride, p.B_dstate_stride = B.stride(0), B.stride(1), B.stride(2)
+    p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
+    p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()
+    p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
+    p.dout, p.chunk_states = dout.data_ptr(), states.data_ptr()
+    p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
+    p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
+    _lib.check(lib.mc_scan_bwd(p, _lib.stream_handle(u.device)), "mc_scan_bwd")
+    return du, ddelta, dA, dB, dC, dD, dz, dbias
+
+
+class SelectiveScanFn(torch.autograd.Function):
+    """Autograd wrapper; mirrors mamba_ssm's SelectiveScanFn contract."""
+
+    @staticmethod
+    def forward(ctx, u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                return_last_state=False):
+        u, delta, z = _last_dim_contig(u), _last_dim_contig(delta), _last_dim_contig(z)
+        squeeze_B, squeeze_C = B.dim() == 3, C.dim() == 3
+        B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
+        A32 = A.float().contiguous()
+        D32 = D.float().contiguous() if D is not None else None
+        bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
+        _check_inputs(u, delta, A32, B, C, D32, z, bias32)
+        need_grad = any(ctx.needs_input_grad[:8])
+        out, states, last = scan_fwd(u, delta, A32, B, C, D32, z, bias32, delta_softplus,
+                                     want_states=need_grad, want_last=return_last_state)
+        if need_grad:
+            ctx.save_for_backward(u, delta, A32, B, C, D32, z, bias32, states)
+        ctx.delta_softplus = delta_softplus
+        ctx.squeeze = (squeeze_B, squeeze_C)
+        ctx.dtypes = (A.dtype, D.dtype if D is not None else None,
+                      delta_bias.dtype if delta_bias is not None else None)
+        ctx.has = (D is not None, z is not None, delta_bias is not None)
+        return (out, last) if return_last_state else out
+
+    @staticmethod
+    def backward(ctx, dout, *args):
+        u, delta, A32, B, C, D32, z, bias32, states = ctx.saved_tensors
+        du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, delta, A32, B, C, D32, z, bias32,
+                                                         ctx.delta_softplus, dout, states)
+        if ctx.squeeze[0]:
+            dB = dB.squeeze(1)
+        if ctx.squeeze[1]:
+            dC = dC.squeeze(1)
+        a_dt, d_dt, b_dt = ctx.dtypes
+        return (du, ddelta, dA.to(a_dt), dB, dC,
+                dD.to(d_dt) if dD is not None else None,
+                dz,
+                dbias.to(b_dt) if dbias is not None else None,
+                None, None)
+
+
+def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                      return_last_state=False):
+    """out = selective_scan(u, delta, A, B, C, D, z, delta_bias, softplus) [, last_state].
+
+    u, delta, z: (B, D, L);  A: (D, N) real;  B, C: (B, N, L) or (B, G, N, L);
+    D, delta_bias: (D,).  ``last_state`` is the fp32 (B, D, N) state after the
+    last position.  Output dtype = u.dtype.
+    """
+    return SelectiveScanFn.apply(u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state)

@@ -1,0 +1,86 @@
+"""CPU-side checks of the C ABI: the library loads, exports every entry point
+include/*.h declares, and the ctypes struct mirrors match the C layout
+(offsets computed by compiling the header with gcc).  No GPU calls."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def _declared_functions():
+    names = set()
+    for h in os.listdir(INCLUDE):
+        if h.endswith(".h"):
+            txt = open(os.path.join(INCLUDE, h)).read()
+            txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            names |= set(re.findall(r"\b(mc_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    declared = _declared_functions()
+    assert declared, "no declarations found"
+    missing = [n for n in declared if not hasattr(lib, n)]
+    assert not missing, f"declared but not exported: {missing}"
+    assert set(declared) <= set(_lib.SYMBOLS), "ctypes SYMBOLS table out of date"
+    assert lib.mc_version().startswith(b"mamba_clip_amd")
+
+
+def test_host_only_entry_points():
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    assert lib.mc_scan_n_chunks(0) == 0
+    assert lib.mc_scan_n_chunks(1) == 1
+    assert lib.mc_scan_n_chunks(32) == 1
+    assert lib.mc_scan_n_chunks(33) == 2
+    assert lib.mc_scan_n_chunks(4096) == 128
+    assert lib.mc_scan_chunk_states_bytes(2, 3, 77, 16) == 2 * 3 * 3 * 16 * 4
+
+
+def test_validation_errors_without_launch():
+    """Bad shapes are rejected on the host before any launch (no GPU needed)."""
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    p = _lib.ScanFwdParams()
+    p.batch, p.dim, p.seqlen, p.dstate, p.n_groups = 1, 6, 8, 16, 4   # dim % groups != 0
+    rc = lib.mc_scan_fwd(ctypes.byref(p), None)
+    assert rc == -3 and b"n_groups" in lib.mc_last_error()
+    p.n_groups, p.dstate = 1, 999
+    assert lib.mc_scan_fwd(ctypes.byref(p), None) == -3
+    p.dstate, p.itype = 16, 7
+    assert lib.mc_scan_fwd(ctypes.byref(p), None) == -2
+    p.itype = 0
+    assert lib.mc_scan_fwd(ctypes.byref(p), None) == -1   # null pointers
+    with pytest.raises(RuntimeError, match="mc_scan_fwd"):
+        _lib.check(lib.mc_scan_fwd(ctypes.byref(p), None), "mc_scan_fwd")
+
+
+@pytest.mark.parametrize("cname,pyname", [("mc_scan_fwd_params", "ScanFwdParams"),
+                                          ("mc_scan_bwd_params", "ScanBwdParams")])
+def test_struct_layout_matches_header(cname, pyname):
+    from mamba_clip_amd import _lib
+    cls = getattr(_lib, pyname)
+    fields = [f for f, _ in cls._fields_]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', "int main(void){",
+           f'printf("size %zu\\n", sizeof({cname}));']
+    src += [f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields]
+    src += ["return 0;}"]
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write("\n".join(src))
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split("\n")
+    got = dict(line.split() for line in out if line)
+    assert int(got["size"]) == ctypes.sizeof(cls)
+    for f in fields:
+        assert int(got[f]) == getattr(cls, f).offset, f

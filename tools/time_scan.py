@@ -1,0 +1,42 @@
+"""Dev tool: time mc_scan_fwd at a given shape with HIP events (not the bench contract)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mamba-clip_amd"))
+from mamba_clip_amd.selective_scan_interface import selective_scan_fn  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--shape", default="64,3072,4096,16")
+ap.add_argument("--dtype", default="bf16")
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--noz", action="store_true")
+args = ap.parse_args()
+Bsz, D, L, N = map(int, args.shape.split(","))
+dt = {"bf16": torch.bfloat16, "f32": torch.float32}[args.dtype]
+dev = "cuda"
+torch.manual_seed(0)
+u = torch.randn(Bsz, D, L, device=dev, dtype=dt)
+delta = (0.5 * torch.randn(Bsz, D, L, device=dev)).to(dt)
+z = None if args.noz else torch.randn(Bsz, D, L, device=dev, dtype=dt)
+A = -torch.exp(torch.log(torch.arange(1, N + 1, dtype=torch.float32, device=dev)).repeat(D, 1))
+Bm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
+Cm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
+Dv = torch.ones(D, device=dev)
+bias = torch.rand(D, device=dev) * 4 - 5
+for _ in range(3):
+    selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
+torch.cuda.synchronize()
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+for _ in range(args.iters):
+    selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
+e.record()
+torch.cuda.synchronize()
+ms = s.elapsed_time(e) / args.iters
+es = u.element_size()
+nbytes = Bsz * D * L * es * (4 if z is not None else 3) + 2 * Bsz * N * L * es + (D * N + 2 * D) * 4
+print(f"shape {args.shape} {args.dtype} z={z is not None}: {ms:.3f} ms  {nbytes / ms / 1e6:.1f} GB/s "
+      f"({nbytes / ms / 1e6 / 8000 * 100:.1f}% of 8 TB/s)")
