@@ -77,6 +77,8 @@ typedef struct mc_scan_fwd_params {
   void* out;
   float* chunk_states;      /* nullable: (batch, dim, n_chunks, dstate) fp32, state at END of each chunk */
   float* last_state;        /* nullable: (batch, dim, dstate) fp32 */
+  void* workspace;          /* >= mc_scan_fwd_workspace_bytes(...) bytes, 16-B aligned */
+  size_t workspace_bytes;
 } mc_scan_fwd_params;
 
 typedef struct mc_scan_bwd_params {
@@ -120,6 +122,9 @@ int32_t mc_scan_n_chunks(int32_t seqlen);
 
 /* bytes of fp32 chunk states the forward writes for a training call */
 size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate);
+
+/* workspace the forward needs (B/C re-laid out as fp32 [batch][group][seqlen][2*dstate']) */
+size_t mc_scan_fwd_workspace_bytes(int32_t batch, int32_t seqlen, int32_t dstate, int32_t n_groups);
 
 /* workspace the backward needs (partial-sum slabs; deterministic reductions) */
 size_t mc_scan_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate,

@@ -1,0 +1,107 @@
+// scan_common.h -- pieces shared by the selective-scan forward and backward.
+#pragma once
+
+#include "mc_common.h"
+#include "../../include/mc_scan.h"
+
+namespace mc {
+namespace scan {
+
+constexpr int kT = MC_SCAN_CHUNK;  // sequence positions per chunk (chunk-state granularity)
+constexpr int kRows = 64;          // channels per workgroup: one wave
+
+// B/C as the recurrence consumes them: fp32, position-major, [b][g][l][2*kNp]
+// (B states 0..kNp-1 then C states; states >= dstate are zero).  Every lane of
+// a wave reads the same position, so one chunk of it is a contiguous block
+// that is staged in LDS once per wave and broadcast-read.
+
+inline int padded_dstate(int dstate) { return dstate <= 8 ? 8 : (dstate <= 16 ? 16 : 32); }
+
+inline size_t bct_bytes(int batch, int seqlen, int dstate, int n_groups) {
+  return (size_t)batch * n_groups * seqlen * 2 * padded_dstate(dstate) * sizeof(float);
+}
+
+// Bijective blockIdx remap so that consecutive logical blocks (same batch /
+// group, sharing B/C) run on one XCD: hardware deals blocks round-robin over
+// the 8 XCDs (speed only -- correctness never depends on placement).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Re-lay B/C (any strides along b/g/n, unit stride along l) into the fp32
+// position-major buffer.  One thread per (b, g, l, j<2kNp).
+template <typename TW, int kNp>
+__global__ __launch_bounds__(256) void bc_relayout_kernel(const TW* __restrict__ B, const TW* __restrict__ C,
+                                                         int64_t B_bs, int64_t B_gs, int64_t B_ns, int64_t C_bs,
+                                                         int64_t C_gs, int64_t C_ns, int batch, int G, int L,
+                                                         int dstate, float* __restrict__ out) {
+  const int64_t total = (int64_t)batch * G * L * 2 * kNp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i % (2 * kNp));
+    const int64_t rest = i / (2 * kNp);
+    const int l = (int)(rest % L);
+    const int64_t bg = rest / L;
+    const int g = (int)(bg % G), b = (int)(bg / G);
+    const bool isC = j >= kNp;
+    const int n = isC ? j - kNp : j;
+    float v = 0.f;
+    if (n < dstate) {
+      const TW* src = isC ? C + (int64_t)b * C_bs + (int64_t)g * C_gs + (int64_t)n * C_ns
+                          : B + (int64_t)b * B_bs + (int64_t)g * B_gs + (int64_t)n * B_ns;
+      v = to_f(src[l]);
+    }
+    out[i] = v;
+  }
+}
+
+template <typename TW>
+inline hipError_t launch_bc_relayout(const void* B, const void* C, int64_t B_bs, int64_t B_gs, int64_t B_ns,
+                                     int64_t C_bs, int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
+                                     float* out, hipStream_t s) {
+  const int np = padded_dstate(dstate);
+  const int64_t total = (int64_t)batch * G * L * 2 * np;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  const TW* b = reinterpret_cast<const TW*>(B);
+  const TW* c = reinterpret_cast<const TW*>(C);
+  if (np == 8)
+    hipLaunchKernelGGL((bc_relayout_kernel<TW, 8>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch,
+                       G, L, dstate, out);
+  else if (np == 16)
+    hipLaunchKernelGGL((bc_relayout_kernel<TW, 16>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns,
+                       batch, G, L, dstate, out);
+  else
+    hipLaunchKernelGGL((bc_relayout_kernel<TW, 32>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns,
+                       batch, G, L, dstate, out);
+  return hipGetLastError();
+}
+
+inline hipError_t relayout_bc(int wtype, const void* B, const void* C, int64_t B_bs, int64_t B_gs, int64_t B_ns,
+                              int64_t C_bs, int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
+                              float* out, hipStream_t s) {
+  if (wtype == MC_DTYPE_F32)
+    return launch_bc_relayout<float>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
+  if (wtype == MC_DTYPE_BF16)
+    return launch_bc_relayout<bf16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
+  return launch_bc_relayout<f16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
+}
+
+// LDS row of one channel for one chunk: kT / VI blocks; block k = {u vector k
+// (16 B = VI steps), delta vector k (16 B)}.  After consuming block k the
+// thread writes y for those VI steps (fp32, 4*VI <= 32 B) over the block, so
+// the y tile costs no extra LDS.  Row stride = data + 16 B: conflict-free
+// ds_read_b128 when every lane reads its own row.
+template <typename TI>
+struct RowLayout {
+  static constexpr int VI = ElemTraits<TI>::kVec;
+  static constexpr int kBlock = 32;
+  static constexpr int kBlocks = kT / VI;
+  static constexpr int kBytes = kBlocks * kBlock;
+  static constexpr int kStride = kBytes + 16;
+};
+
+int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who);
+bool vec_ok(const void* p, int64_t s0, int64_t s1, int64_t s2, int elem_bytes);
+
+}  // namespace scan
+}  // namespace mc

@@ -7,74 +7,66 @@
 //   y_t  = sum_n C[b,g,n,t] * x_t[n]  (+ D[d] * u_t)  (* silu(z_t))
 //
 // Design (DESIGN.md "scan_fwd"):
-//  * One thread owns one (b, d) channel and keeps all dstate states in
-//    registers, walking the sequence in chunks of kT = 32 positions.  This is
-//    the work-optimal form of the recurrence (no parallel-prefix overhead);
-//    B*D channels give >= 3 waves/SIMD at the benchmark shapes.
-//  * A workgroup = up to 256 channels of ONE (batch, group), so B_t / C_t are
-//    wave-uniform: they are staged once per chunk in LDS as fp32 [t][n] and
-//    read with broadcast ds_read_b128.
-//  * u / delta tiles are moved HBM -> registers with fully coalesced 16-byte
-//    loads along the sequence (64-B row segments), written to LDS rows, and
-//    each thread then reads back its own row (bank-conflict-free: row stride
-//    = 144 B for 16-bit inputs).  The next chunk's loads are issued right after
-//    the LDS write, so their latency hides under this chunk's recurrence.
-//  * y (+D u) is written back over the thread's own (already consumed) LDS
-//    row in fp32; a cooperative pass then applies the z gate with coalesced z
-//    loads and out stores.  HBM traffic = the algorithmic bytes.
+//  * One lane owns one (b, d) channel and keeps its dstate states in VGPRs,
+//    walking the sequence in chunks of kT = 32 positions: the work-optimal
+//    form of the recurrence (no parallel-prefix overhead).  B*D channels give
+//    thousands of waves at the benchmark shapes.
+//  * A workgroup is ONE wave = 64 channels of one (batch, group): no
+//    inter-wave barriers, fine-grained grid (no tail), XCD-aware ordering so
+//    the waves of one batch share an XCD's L2.
+//  * B_t / C_t are wave-uniform: a pre-pass re-lays them out as fp32
+//    [b][g][l][2N]; each chunk's slice is staged in LDS and read with
+//    broadcast ds_read_b128 (one address for all lanes).
+//  * u / delta tiles move HBM -> registers (next chunk, prefetched under the
+//    current chunk's recurrence) -> LDS with fully coalesced 16-B loads along
+//    the sequence; each lane then reads back its own row (conflict-free).
+//    y (+D u) is written back over the consumed row in fp32, and a
+//    cooperative pass applies the z gate with coalesced z loads / out stores.
 //  * exp(dt*A) = exp2(dt * A*log2e) on v_exp_f32.
-#include "mc_common.h"
-#include "../../include/mc_scan.h"
+#include "scan_common.h"
+
 
 namespace mc {
 namespace scan {
 
-constexpr int kT = MC_SCAN_CHUNK;  // sequence positions per chunk
-constexpr int kMaxRows = 256;      // channels per workgroup
-
-// LDS row of one channel for one chunk: kT/4 blocks, block k = {u[4k..4k+3],
-// delta[4k..4k+3]} (2 x 4 elements).  After the thread has consumed block k
-// it writes y[4k..4k+3] (fp32, 16 B) over the block's first 16 bytes, so the
-// y tile needs no extra LDS.
-template <typename TI>
-struct RowLayout {
-  static constexpr int kHalf = 4 * (int)sizeof(TI);         // 4 elements of one array
-  static constexpr int kBlock = 2 * kHalf;                   // >= 16 B (room for 4 fp32 y)
-  static constexpr int kBytes = (kT / 4) * kBlock;
-  static constexpr int kStride = kBytes + 16;                // pad: conflict-free row reads
-};
-
 struct FwdArgs {
-  int batch, dim, seqlen, dstate, n_groups, n_chunks;
+  int batch, dim, seqlen, dstate, n_groups, n_chunks, nblk, total_blocks;
   int softplus;
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, o_bs, o_ds;
-  int64_t B_bs, B_gs, B_ns, C_bs, C_gs, C_ns;
-  const void* u; const void* delta; const float* A; const void* B; const void* C;
+  const void* u; const void* delta; const float* A; const float* bct;
   const float* D; const void* z; const float* delta_bias;
   void* out; float* chunk_states; float* last_state;
 };
 
-template <typename TI, typename TW, int kN, bool kAligned>
-__global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) {
-  using L = RowLayout<TI>;
-  constexpr int VI = ElemTraits<TI>::kVec;      // elements per 16-B vector (inputs)
-  constexpr int VW = ElemTraits<TW>::kVec;      // elements per 16-B vector (B/C)
-  constexpr int kVPR = kT / VI;                 // vectors per row segment
-  constexpr int kBCRow = kT / VW;               // vectors per (n) row of a B/C chunk
-  constexpr int kBCVecs = kN * kBCRow;          // vectors in one B (or C) chunk tile
-  constexpr int kBCPer = (2 * kBCVecs + 63) / 64;  // per thread, sized for a 64-row workgroup
+// waves per SIMD the register budget is sized for (16-bit I/O at dstate <= 16:
+// <= 128 VGPRs, no spill -> 4 waves/SIMD; wider variants get 2)
+// Register budget: 2 waves/SIMD (<= 256 VGPRs).  Measured on MI355X at C4
+// (B=64, D=3072, L=4096, N=16, bf16): 4-step groups at 2 waves/SIMD beat
+// 2-step groups at 3-4 waves/SIMD (the hoisted broadcast B/C reads of a
+// group need ~128 VGPRs) and the SGPR (scalar-load) B/C variant, whose
+// SGPR-operand VALU issues at ~0.6x the VGPR rate (tools/ubench/valu_rate.hip).
+template <typename TI, int kN>
+constexpr int fwd_min_waves() { return 2; }
+
+template <typename TI, int kN, bool kAligned>
+__global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_kernel(const FwdArgs a) {
+  using RL = RowLayout<TI>;
+  constexpr int kG = 4;                         // steps per group in the recurrence loop
+  constexpr int VI = RL::VI;                    // elements per 16-B vector
+  constexpr int kVPR = kT / VI;                 // vectors per row segment per array
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int rows = blockDim.x;
   char* rowbuf = smem;
-  float* bc = reinterpret_cast<float*>(smem + rows * L::kStride);  // [kT][2*kN]: B then C
+  float* bcl = reinterpret_cast<float*>(smem + kRows * RL::kStride);   // [kT][2kN] (mode 1)
 
-  const int tid = threadIdx.x;
-  const int b = blockIdx.z;
-  const int g = blockIdx.y;
+  const int lane = threadIdx.x;
+  const int lin = xcd_remap(blockIdx.x, a.total_blocks);
+  const int dblk = lin % a.nblk;
+  const int bg = lin / a.nblk;
+  const int g = bg % a.n_groups, b = bg / a.n_groups;
   const int H = a.dim / a.n_groups;
-  const int dbase = g * H + blockIdx.x * rows;
-  const int nrows = min(rows, H - (int)blockIdx.x * rows);
+  const int dbase = g * H + dblk * kRows;
+  const int nrows = min(kRows, H - dblk * kRows);
   const int L_ = a.seqlen;
   const bool hasZ = a.z != nullptr;
   const bool softplus = a.softplus != 0;
@@ -83,12 +75,10 @@ __global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) 
   const TI* __restrict__ dl = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs;
   const TI* __restrict__ zp = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs;
   TI* __restrict__ out = reinterpret_cast<TI*>(a.out) + (int64_t)b * a.o_bs;
-  const TW* __restrict__ Bp = reinterpret_cast<const TW*>(a.B) + (int64_t)b * a.B_bs + (int64_t)g * a.B_gs;
-  const TW* __restrict__ Cp = reinterpret_cast<const TW*>(a.C) + (int64_t)b * a.C_bs + (int64_t)g * a.C_gs;
 
   // ---- per-channel constants
-  const int my_d = dbase + tid;
-  const bool my_ok = tid < nrows;
+  const int my_d = dbase + lane;
+  const bool my_ok = lane < nrows;
   float A2[kN];
 #pragma unroll
   for (int n = 0; n < kN; ++n)
@@ -100,20 +90,22 @@ __global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) 
 #pragma unroll
   for (int n = 0; n < kN; ++n) x[n] = 0.f;
 
-  // ---- cooperative tile movers.  Vector j = tid + k*rows -> (row j / kVPR,
-  // col j % kVPR): kVPR consecutive lanes cover one 64-B row segment.
-  // Rows past the group end are clamped onto a valid row (loaded, never stored).
-  uint4 pu[kVPR], pd[kVPR], pbc[kBCPer];
-
-  auto load_tiles = [&](int l0) {
+  // ---- register prefetch of the next chunk (issued before this chunk's
+  // recurrence, consumed after it): u / delta vectors + the B/C chunk.
+  constexpr int kBCVec = kT * 2 * kN / 4;                 // float4s in one B/C chunk
+  constexpr int kBCPer = (kBCVec + kRows - 1) / kRows;
+  uint4 pu[kVPR], pd[kVPR];
+  float4 pbc[kBCPer];
+  auto load_regs = [&](int l0) {
     const bool full = kAligned && (l0 + kT <= L_);
 #pragma unroll
     for (int k = 0; k < kVPR; ++k) {
-      const int j = tid + k * rows;
-      const int r = min(j / kVPR, nrows - 1), c = j % kVPR;
+      const int j = lane + k * kRows;
+      const int r = j / kVPR, c = j % kVPR;
+      const int rr = min(r, nrows - 1);   // rows past the group end: load a valid row, never stored
       const int col0 = l0 + c * VI;
-      const TI* su = u + (int64_t)(dbase + r) * a.u_ds + col0;
-      const TI* sd = dl + (int64_t)(dbase + r) * a.dt_ds + col0;
+      const TI* su = u + (int64_t)(dbase + rr) * a.u_ds + col0;
+      const TI* sd = dl + (int64_t)(dbase + rr) * a.dt_ds + col0;
       if (full) {
         pu[k] = ld16(su);
         pd[k] = ld16(sd);
@@ -123,108 +115,104 @@ __global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) 
         pd[k] = ld16_masked(sd, nv);
       }
     }
+    {
+      const float4* src = reinterpret_cast<const float4*>(a.bct + ((int64_t)bg * L_ + l0) * (2 * kN));
+      const int nvec = min(kT, L_ - l0) * (2 * kN) / 4;
 #pragma unroll
-    for (int k = 0; k < kBCPer; ++k) {
-      const int j = tid + k * rows;
-      const bool isC = j >= kBCVecs;
-      const int jj = isC ? j - kBCVecs : j;
-      const int n = min(jj / kBCRow, a.dstate - 1), c = jj % kBCRow;
-      const int col0 = l0 + c * VW;
-      const TW* src = (isC ? Cp + (int64_t)n * a.C_ns : Bp + (int64_t)n * a.B_ns) + col0;
-      if (j < 2 * kBCVecs) {
-        if (full) pbc[k] = ld16(src);
-        else pbc[k] = ld16_masked(src, max(0, min(VW, L_ - col0)));
-      }
-    }
-  };
-  auto store_tiles_lds = [&]() {
-#pragma unroll
-    for (int k = 0; k < kVPR; ++k) {
-      const int j = tid + k * rows;
-      const int r = j / kVPR, c = j % kVPR;
-      char* row = rowbuf + r * L::kStride;
-      if constexpr (L::kHalf == 16) {   // fp32: one vector = one half-block
-        char* blk = row + c * L::kBlock;
-        st16(blk, pu[k]);
-        st16(blk + L::kHalf, pd[k]);
-      } else {                          // 16-bit: one vector = two half-blocks
-        char* blk = row + 2 * c * L::kBlock;
-        *reinterpret_cast<uint2*>(blk) = make_uint2(pu[k].x, pu[k].y);
-        *reinterpret_cast<uint2*>(blk + L::kHalf) = make_uint2(pd[k].x, pd[k].y);
-        *reinterpret_cast<uint2*>(blk + L::kBlock) = make_uint2(pu[k].z, pu[k].w);
-        *reinterpret_cast<uint2*>(blk + L::kBlock + L::kHalf) = make_uint2(pd[k].z, pd[k].w);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kBCPer; ++k) {
-      const int j = tid + k * rows;
-      if (j < 2 * kBCVecs) {
-        const bool isC = j >= kBCVecs;
-        const int jj = isC ? j - kBCVecs : j;
-        const int n = jj / kBCRow, c = jj % kBCRow;
-        float* dst = bc + (c * VW) * (2 * kN) + (isC ? kN : 0) + n;
-        const bool live = n < a.dstate;   // padded states read B = C = 0
-#pragma unroll
-        for (int e = 0; e < VW; ++e) dst[e * 2 * kN] = live ? elem_f<TW>(pbc[k], e) : 0.f;
+      for (int k = 0; k < kBCPer; ++k) {
+        const int v = lane + k * kRows;
+        pbc[k] = v < nvec ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   };
 
-  load_tiles(0);
+  load_regs(0);
   for (int ch = 0; ch < a.n_chunks; ++ch) {
     const int l0 = ch * kT;
-    __syncthreads();  // previous chunk's gate pass is done with rowbuf / bc
-    store_tiles_lds();
-    __syncthreads();
-    if (ch + 1 < a.n_chunks) load_tiles(l0 + kT);  // in flight during the recurrence
+    const bool full = kAligned && (l0 + kT <= L_);
 
-    // ---- the recurrence over this chunk, one channel per thread
-    if (my_ok) {
-      char* row = rowbuf + tid * L::kStride;
-#pragma unroll 2
-      for (int t4 = 0; t4 < kT; t4 += 4) {
-        char* blk = row + (t4 / 4) * L::kBlock;
-        uint4 bu, bd;   // elements 0..3 of each
-        if constexpr (L::kHalf == 16) {
-          bu = ld16(blk);
-          bd = ld16(blk + L::kHalf);
-        } else {
-          const uint4 q = ld16(blk);
-          bu = make_uint4(q.x, q.y, 0u, 0u);
-          bd = make_uint4(q.z, q.w, 0u, 0u);
-        }
-        float yv[4];
+    // ---- stage u / delta (vector j = lane + k*64 -> row j / kVPR, col j % kVPR) and B/C
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
-          const int t = t4 + tt;
-          const float uv = elem_f<TI>(bu, tt);
-          const float dr = elem_f<TI>(bd, tt) + biasv;
-          float dt = softplus ? softplus_f(dr) : dr;
-          dt = (l0 + t < L_) ? dt : 0.f;  // past the end: state frozen
-          const float du = dt * uv;
-          const float4* bct = reinterpret_cast<const float4*>(bc + t * 2 * kN);
-          float y = 0.f;
+    for (int k = 0; k < kVPR; ++k) {
+      const int j = lane + k * kRows;
+      const int r = j / kVPR, c = j % kVPR;
+      char* blk = rowbuf + r * RL::kStride + c * RL::kBlock;
+      st16(blk, pu[k]);
+      st16(blk + 16, pd[k]);
+    }
+    {
 #pragma unroll
-          for (int n4 = 0; n4 < kN / 4; ++n4) {
-            const float4 bq = bct[n4];
-            const float4 cq = bct[kN / 4 + n4];
-#define MC_STEP(i, BB, CC)                                \
-            {                                             \
-              const float dA = fast_exp2(dt * A2[n4 * 4 + i]); \
-              x[n4 * 4 + i] = fmaf(dA, x[n4 * 4 + i], du * BB); \
-              y = fmaf(CC, x[n4 * 4 + i], y);             \
-            }
-            MC_STEP(0, bq.x, cq.x)
-            MC_STEP(1, bq.y, cq.y)
-            MC_STEP(2, bq.z, cq.z)
-            MC_STEP(3, bq.w, cq.w)
-#undef MC_STEP
-          }
-          yv[tt] = fmaf(Dv, uv, y);
-        }
-        *reinterpret_cast<float4*>(blk) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+      for (int k = 0; k < kBCPer; ++k) {
+        const int v = lane + k * kRows;
+        if (v < kBCVec) reinterpret_cast<float4*>(bcl)[v] = pbc[k];
       }
-      if (a.chunk_states) {
+    }
+    __syncthreads();
+    if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
+
+    // ---- the recurrence over this chunk, one channel per lane.  Steps go
+    // in groups of kG: read the group's u / delta (kG elements each), run
+    // kG steps, write the kG fp32 y values back over exactly those bytes.
+    {
+      char* row = rowbuf + lane * RL::kStride;
+#pragma unroll 1
+      for (int t0 = 0; t0 < kT; t0 += kG) {
+        char* pu = row + (t0 / VI) * RL::kBlock + (t0 % VI) * (int)sizeof(TI);
+        char* pd = pu + 16;
+        float uu[kG], dd[kG];
+        {
+          constexpr int kB = kG * (int)sizeof(TI);   // bytes of one array in this group
+          uint4 qa, qb;
+          if constexpr (kB == 16) { qa = ld16(pu); qb = ld16(pd); }
+          else if constexpr (kB == 8) {
+            const uint2 a2 = *reinterpret_cast<const uint2*>(pu), b2 = *reinterpret_cast<const uint2*>(pd);
+            qa = make_uint4(a2.x, a2.y, 0u, 0u); qb = make_uint4(b2.x, b2.y, 0u, 0u);
+          } else if constexpr (kB == 4) {
+            qa = make_uint4(*reinterpret_cast<const uint32_t*>(pu), 0u, 0u, 0u);
+            qb = make_uint4(*reinterpret_cast<const uint32_t*>(pd), 0u, 0u, 0u);
+          } else {
+            static_assert(kB >= 4, "group must cover >= 4 bytes per array");
+          }
+#pragma unroll
+          for (int e = 0; e < kG; ++e) { uu[e] = elem_f<TI>(qa, e); dd[e] = elem_f<TI>(qb, e); }
+        }
+        float yv[kG];
+#pragma unroll
+        for (int e = 0; e < kG; ++e) {
+          const int t = l0 + t0 + e;
+          const float uv = uu[e];
+          const float dr = dd[e] + biasv;
+          float dt = softplus ? softplus_f(dr) : dr;
+          dt = (t < L_) ? dt : 0.f;  // past the end: state frozen
+          const float du = dt * uv;
+          float y = 0.f;
+          {
+            const float4* bc4 = reinterpret_cast<const float4*>(bcl + (t0 + e) * (2 * kN));
+#pragma unroll
+            for (int n4 = 0; n4 < kN / 4; ++n4) {
+              const float4 bq = bc4[n4], cq = bc4[kN / 4 + n4];
+              const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, cc[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float dA = fast_exp2(dt * A2[4 * n4 + i]);
+                x[4 * n4 + i] = fmaf(dA, x[4 * n4 + i], du * bb[i]);
+                y = fmaf(cc[i], x[4 * n4 + i], y);
+              }
+            }
+          }
+          yv[e] = fmaf(Dv, uv, y);
+        }
+        // y[0..kG/2) -> the u bytes, y[kG/2..kG) -> the delta bytes of this group
+        if constexpr (kG == 4) {
+          *reinterpret_cast<float2*>(pu) = make_float2(yv[0], yv[1]);
+          *reinterpret_cast<float2*>(pd) = make_float2(yv[2], yv[3]);
+        } else {
+          static_assert(kG == 2, "kG in {2, 4}");
+          *reinterpret_cast<float*>(pu) = yv[0];
+          *reinterpret_cast<float*>(pd) = yv[1];
+        }
+      }
+      if (a.chunk_states && my_ok) {
         float* cs = a.chunk_states + (((int64_t)b * a.dim + my_d) * a.n_chunks + ch) * a.dstate;
         if ((a.dstate & 3) == 0) {
 #pragma unroll
@@ -240,35 +228,38 @@ __global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) 
     }
     __syncthreads();
 
-    // ---- gate + store: coalesced along the sequence
-    const bool full = kAligned && (l0 + kT <= L_);
+    // ---- gate + store, coalesced along the sequence (same vector mapping)
 #pragma unroll
     for (int k = 0; k < kVPR; ++k) {
-      const int j = tid + k * rows;
+      const int j = lane + k * kRows;
       const int r = j / kVPR, c = j % kVPR;
       const int col0 = l0 + c * VI;
-      const char* yrow = rowbuf + r * L::kStride;
-      const TI* zsrc = zp + (int64_t)(dbase + min(r, nrows - 1)) * a.z_ds + col0;
       const int nv = max(0, min(VI, L_ - col0));
-      uint4 zv = make_uint4(0u, 0u, 0u, 0u);
-      if (hasZ) zv = full ? ld16(zsrc) : ld16_masked(zsrc, nv);
       float o[VI];
+      // y of step s (within the chunk) lives in group s / kG: first half of the
+      // group's y values at the u bytes, second half at the delta bytes.
 #pragma unroll
-      for (int e4 = 0; e4 < VI; e4 += 4) {
-        const float4 yq = *reinterpret_cast<const float4*>(yrow + (c * (VI / 4) + e4 / 4) * L::kBlock);
-        o[e4 + 0] = yq.x; o[e4 + 1] = yq.y; o[e4 + 2] = yq.z; o[e4 + 3] = yq.w;
+      for (int e = 0; e < VI; ++e) {
+        const int st = c * VI + e;
+        const int g0 = st - st % kG;
+        const int ie = st % kG;
+        const char* pu = rowbuf + r * RL::kStride + (g0 / VI) * RL::kBlock + (g0 % VI) * (int)sizeof(TI);
+        o[e] = reinterpret_cast<const float*>(ie < kG / 2 ? pu : pu + 16)[ie % (kG / 2)];
       }
       if (hasZ) {
+        const TI* zs = zp + (int64_t)(dbase + min(r, nrows - 1)) * a.z_ds + col0;
+        const uint4 zq = full ? ld16(zs) : ld16_masked(zs, nv);
 #pragma unroll
-        for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(zv, e));
+        for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(zq, e));
       }
-      const uint4 ov = pack_f<TI>(o);
-      TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
       if (r < nrows) {
+        TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
+        const uint4 ov = pack_f<TI>(o);
         if (full) st16(dst, ov);
         else st16_masked(dst, ov, nv);
       }
     }
+    __syncthreads();  // next chunk's staging overwrites the rows
   }
 
   if (a.last_state && my_ok) {
@@ -280,26 +271,41 @@ __global__ __launch_bounds__(kMaxRows, 2) void scan_fwd_kernel(const FwdArgs a) 
 }
 
 // ------------------------------------------------------------------ host dispatch
-template <typename TI, typename TW, int kN>
+template <typename TI, int kN>
 static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
-  const int H = a.dim / a.n_groups;
-  const int rows = H >= kMaxRows ? kMaxRows : ((H + 63) / 64) * 64;
-  dim3 grid((H + rows - 1) / rows, a.n_groups, a.batch);
-  const size_t lds = (size_t)rows * RowLayout<TI>::kStride + (size_t)kT * 2 * kN * sizeof(float);
+  const size_t lds = (size_t)kRows * RowLayout<TI>::kStride + (size_t)kT * 2 * kN * 4;
   if (aligned)
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, TW, kN, true>), grid, dim3(rows), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, TW, kN, false>), grid, dim3(rows), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, false>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }
 
-template <typename TI, typename TW>
+template <typename TI>
 static int launch_fwd_t(const FwdArgs& a, bool aligned, hipStream_t s) {
-  if (a.dstate <= 8) return launch_fwd_n<TI, TW, 8>(a, aligned, s);
-  if (a.dstate <= 16) return launch_fwd_n<TI, TW, 16>(a, aligned, s);
-  return launch_fwd_n<TI, TW, 32>(a, aligned, s);
+  const int np = padded_dstate(a.dstate);
+  if (np == 8) return launch_fwd_n<TI, 8>(a, aligned, s);
+  if (np == 16) return launch_fwd_n<TI, 16>(a, aligned, s);
+  return launch_fwd_n<TI, 32>(a, aligned, s);
+}
+
+int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who) {
+  MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0, MC_ERR_SHAPE, "%s: bad shape batch=%d dim=%d seqlen=%d", who,
+           batch, dim, seqlen);
+  MC_CHECK(dstate >= 1 && dstate <= MC_SCAN_MAX_DSTATE, MC_ERR_SHAPE, "%s: dstate=%d must be in [1, %d]", who,
+           dstate, MC_SCAN_MAX_DSTATE);
+  MC_CHECK(n_groups >= 1 && dim % n_groups == 0, MC_ERR_SHAPE, "%s: dim=%d not divisible by n_groups=%d", who,
+           dim, n_groups);
+  MC_CHECK(itype >= MC_DTYPE_F32 && itype <= MC_DTYPE_F16, MC_ERR_DTYPE, "%s: bad input dtype %d", who, itype);
+  MC_CHECK(wtype >= MC_DTYPE_F32 && wtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "%s: bad weight dtype %d", who, wtype);
+  return MC_OK;
+}
+
+bool vec_ok(const void* p, int64_t s0, int64_t s1, int64_t s2, int elem_bytes) {
+  const int64_t v = 16 / elem_bytes;
+  return p == nullptr || (aligned16(p) && s0 % v == 0 && s1 % v == 0 && s2 % v == 0);
 }
 
 }  // namespace scan
@@ -315,65 +321,52 @@ extern "C" size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t
   return (size_t)batch * dim * mc_scan_n_chunks(seqlen) * dstate * sizeof(float);
 }
 
-int mc_validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype,
-                       const char* who) {
-  MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0, MC_ERR_SHAPE, "%s: bad shape batch=%d dim=%d seqlen=%d", who,
-           batch, dim, seqlen);
-  MC_CHECK(dstate >= 1 && dstate <= MC_SCAN_MAX_DSTATE, MC_ERR_SHAPE, "%s: dstate=%d must be in [1, %d]", who,
-           dstate, MC_SCAN_MAX_DSTATE);
-  MC_CHECK(n_groups >= 1 && dim % n_groups == 0, MC_ERR_SHAPE, "%s: dim=%d not divisible by n_groups=%d", who,
-           dim, n_groups);
-  MC_CHECK(itype >= MC_DTYPE_F32 && itype <= MC_DTYPE_F16, MC_ERR_DTYPE, "%s: bad input dtype %d", who, itype);
-  MC_CHECK(wtype >= MC_DTYPE_F32 && wtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "%s: bad weight dtype %d", who, wtype);
-  return MC_OK;
-}
-
-static bool vec_ok(const void* p, int64_t s0, int64_t s1, int64_t s2, int elem_bytes) {
-  const int64_t v = 16 / elem_bytes;
-  return p == nullptr || (aligned16(p) && s0 % v == 0 && s1 % v == 0 && s2 % v == 0);
+extern "C" size_t mc_scan_fwd_workspace_bytes(int32_t batch, int32_t seqlen, int32_t dstate, int32_t n_groups) {
+  return bct_bytes(batch, seqlen, dstate, n_groups);
 }
 
 extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_scan_fwd: null params");
-  int rc = mc_validate_common(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups, p->itype, p->wtype,
-                              "mc_scan_fwd");
+  int rc = validate_common(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups, p->itype, p->wtype, "mc_scan_fwd");
   if (rc) return rc;
   MC_CHECK(p->u && p->delta && p->A && p->B && p->C && p->out, MC_ERR_INVALID,
            "mc_scan_fwd: u, delta, A, B, C and out must be non-null");
+  hipStream_t s = (hipStream_t)stream;
   if (p->batch == 0 || p->seqlen == 0) {
     // nothing to scan; a zero-length sequence leaves the state at zero
-    if (p->last_state)
-      (void)hipMemsetAsync(p->last_state, 0, (size_t)p->batch * p->dim * p->dstate * 4, (hipStream_t)stream);
+    if (p->last_state) (void)hipMemsetAsync(p->last_state, 0, (size_t)p->batch * p->dim * p->dstate * 4, s);
     return MC_OK;
   }
+  const size_t need = bct_bytes(p->batch, p->seqlen, p->dstate, p->n_groups);
+  MC_CHECK(p->workspace && p->workspace_bytes >= need && aligned16(p->workspace), MC_ERR_WORKSPACE,
+           "mc_scan_fwd: workspace must be >= %zu bytes and 16-B aligned (got %zu)", need, p->workspace_bytes);
+
+  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
+                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
+                             p->seqlen, p->dstate, reinterpret_cast<float*>(p->workspace), s);
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
+
   FwdArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
   a.n_chunks = mc_scan_n_chunks(p->seqlen);
+  const int H = p->dim / p->n_groups;
+  a.nblk = (H + kRows - 1) / kRows;
+  a.total_blocks = p->batch * p->n_groups * a.nblk;
   a.softplus = p->delta_softplus;
   a.u_bs = p->u_batch_stride; a.u_ds = p->u_dim_stride;
   a.dt_bs = p->delta_batch_stride; a.dt_ds = p->delta_dim_stride;
   a.z_bs = p->z_batch_stride; a.z_ds = p->z_dim_stride;
   a.o_bs = p->out_batch_stride; a.o_ds = p->out_dim_stride;
-  a.B_bs = p->B_batch_stride; a.B_gs = p->B_group_stride; a.B_ns = p->B_dstate_stride;
-  a.C_bs = p->C_batch_stride; a.C_gs = p->C_group_stride; a.C_ns = p->C_dstate_stride;
-  a.u = p->u; a.delta = p->delta; a.A = p->A; a.B = p->B; a.C = p->C; a.D = p->D; a.z = p->z;
-  a.delta_bias = p->delta_bias; a.out = p->out; a.chunk_states = p->chunk_states; a.last_state = p->last_state;
+  a.u = p->u; a.delta = p->delta; a.A = p->A; a.bct = reinterpret_cast<const float*>(p->workspace);
+  a.D = p->D; a.z = p->z; a.delta_bias = p->delta_bias;
+  a.out = p->out; a.chunk_states = p->chunk_states; a.last_state = p->last_state;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
-  const int wb = p->wtype == MC_DTYPE_F32 ? 4 : 2;
   const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
                        vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
-                       vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
-                       vec_ok(p->B, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride, wb) &&
-                       vec_ok(p->C, p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, wb);
-  hipStream_t s = (hipStream_t)stream;
-  const int it = p->itype, wt = p->wtype;
-  if (it == MC_DTYPE_F32 && wt == MC_DTYPE_F32) return launch_fwd_t<float, float>(a, aligned, s);
-  if (it == MC_DTYPE_F32 && wt == MC_DTYPE_BF16) return launch_fwd_t<float, bf16_t>(a, aligned, s);
-  if (it == MC_DTYPE_BF16 && wt == MC_DTYPE_BF16) return launch_fwd_t<bf16_t, bf16_t>(a, aligned, s);
-  if (it == MC_DTYPE_BF16 && wt == MC_DTYPE_F32) return launch_fwd_t<bf16_t, float>(a, aligned, s);
-  if (it == MC_DTYPE_F16 && wt == MC_DTYPE_F16) return launch_fwd_t<f16_t, f16_t>(a, aligned, s);
-  if (it == MC_DTYPE_F16 && wt == MC_DTYPE_F32) return launch_fwd_t<f16_t, float>(a, aligned, s);
-  MC_CHECK(false, MC_ERR_DTYPE, "mc_scan_fwd: unsupported dtype combination itype=%d wtype=%d", it, wt);
+                       vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib);
+  if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
+  if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
+  return launch_fwd_t<f16_t>(a, aligned, s);
 }

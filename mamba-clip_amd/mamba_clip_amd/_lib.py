@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmamba_clip_amd.so")
+# MAMBA_CLIP_AMD_LIB overrides the path (dev A/B builds only)
+LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB", os.path.join(_HERE, "libmamba_clip_amd.so"))
 
 MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16 = 0, 1, 2
 MC_SCAN_CHUNK = 32
@@ -31,6 +32,7 @@ class ScanFwdParams(ctypes.Structure):
         ("u", c_vp), ("delta", c_vp), ("A", c_fp), ("B", c_vp), ("C", c_vp),
         ("D", c_fp), ("z", c_vp), ("delta_bias", c_fp),
         ("out", c_vp), ("chunk_states", c_fp), ("last_state", c_fp),
+        ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
     ]
 
 
@@ -59,6 +61,7 @@ SYMBOLS = {
     "mc_version": (ctypes.c_char_p, []),
     "mc_scan_n_chunks": (c_i32, [c_i32]),
     "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
+    "mc_scan_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd": (ctypes.c_int, [ctypes.POINTER(ScanFwdParams), c_vp]),
     "mc_scan_bwd": (ctypes.c_int, [ctypes.POINTER(ScanBwdParams), c_vp]),

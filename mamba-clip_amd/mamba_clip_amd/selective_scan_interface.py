@@ -39,8 +39,8 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
         raise RuntimeError("selective_scan_fn: complex A is not supported")
     if delta.dtype != u.dtype or (z is not None and z.dtype != u.dtype):
         raise RuntimeError("selective_scan_fn: u, delta and z must share a dtype")
-    if B.dtype not in (torch.float32, u.dtype) or C.dtype != B.dtype:
-        raise RuntimeError("selective_scan_fn: B/C must be float32 or the input dtype, and equal")
+    if C.dtype != B.dtype:
+        raise RuntimeError("selective_scan_fn: B and C must share a dtype")
     batch, dim, L = u.shape
     if delta.shape != u.shape or (z is not None and z.shape != u.shape):
         raise RuntimeError("selective_scan_fn: u, delta, z shape mismatch")
@@ -82,6 +82,9 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()
     p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
     p.out, p.chunk_states, p.last_state = out.data_ptr(), _lib.ptr(states), _lib.ptr(last)
+    ws_bytes = lib.mc_scan_fwd_workspace_bytes(batch, L, dstate, G)
+    ws = torch.empty(max(ws_bytes, 1), device=u.device, dtype=torch.uint8)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
     _lib.check(lib.mc_scan_fwd(p, _lib.stream_handle(u.device)), "mc_scan_fwd")
     if want_last and states is not None:
         last = states[:, :, -1, :] if nch > 0 else torch.zeros(batch, dim, dstate, device=u.device)
