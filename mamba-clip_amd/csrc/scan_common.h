@@ -7,7 +7,8 @@
 namespace mc {
 namespace scan {
 
-constexpr int kT = MC_SCAN_CHUNK;  // sequence positions per chunk (chunk-state granularity)
+constexpr int kT = 32;             // sequence positions per forward tile
+constexpr int kS = MC_SCAN_CHUNK;  // positions per saved chunk state (16)
 constexpr int kRows = 64;          // channels per workgroup: one wave
 
 // B/C as the recurrence consumes them: fp32, position-major, [b][g][l][2*kNp]

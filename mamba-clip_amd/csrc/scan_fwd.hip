@@ -30,7 +30,7 @@ namespace mc {
 namespace scan {
 
 struct FwdArgs {
-  int batch, dim, seqlen, dstate, n_groups, n_chunks, nblk, total_blocks;
+  int batch, dim, seqlen, dstate, n_groups, n_chunks, n_states, nblk, total_blocks;
   int softplus;
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, o_bs, o_ds;
   const void* u; const void* delta; const float* A; const float* bct;
@@ -203,6 +203,22 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
           yv[e] = fmaf(Dv, uv, y);
         }
         // y[0..kG/2) -> the u bytes, y[kG/2..kG) -> the delta bytes of this group
+        if (a.chunk_states && my_ok && ((t0 + kG) % kS) == 0) {
+          const int sc = (l0 + t0 + kG) / kS - 1;   // saved-state index: state after position sc*kS + kS - 1
+          if (sc < a.n_states) {
+            float* cs = a.chunk_states + (((int64_t)b * a.dim + my_d) * a.n_states + sc) * a.dstate;
+            if ((a.dstate & 3) == 0) {
+#pragma unroll
+              for (int n4 = 0; n4 < kN / 4; ++n4)
+                if (n4 * 4 < a.dstate)
+                  reinterpret_cast<float4*>(cs)[n4] = make_float4(x[4 * n4], x[4 * n4 + 1], x[4 * n4 + 2], x[4 * n4 + 3]);
+            } else {
+#pragma unroll
+              for (int n = 0; n < kN; ++n)
+                if (n < a.dstate) cs[n] = x[n];
+            }
+          }
+        }
         if constexpr (kG == 4) {
           *reinterpret_cast<float2*>(pu) = make_float2(yv[0], yv[1]);
           *reinterpret_cast<float2*>(pd) = make_float2(yv[2], yv[3]);
@@ -210,19 +226,6 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
           static_assert(kG == 2, "kG in {2, 4}");
           *reinterpret_cast<float*>(pu) = yv[0];
           *reinterpret_cast<float*>(pd) = yv[1];
-        }
-      }
-      if (a.chunk_states && my_ok) {
-        float* cs = a.chunk_states + (((int64_t)b * a.dim + my_d) * a.n_chunks + ch) * a.dstate;
-        if ((a.dstate & 3) == 0) {
-#pragma unroll
-          for (int n4 = 0; n4 < kN / 4; ++n4)
-            if (n4 * 4 < a.dstate)
-              reinterpret_cast<float4*>(cs)[n4] = make_float4(x[4 * n4], x[4 * n4 + 1], x[4 * n4 + 2], x[4 * n4 + 3]);
-        } else {
-#pragma unroll
-          for (int n = 0; n < kN; ++n)
-            if (n < a.dstate) cs[n] = x[n];
         }
       }
     }
@@ -315,7 +318,7 @@ bool vec_ok(const void* p, int64_t s0, int64_t s1, int64_t s2, int elem_bytes) {
 using namespace mc;
 using namespace mc::scan;
 
-extern "C" int32_t mc_scan_n_chunks(int32_t seqlen) { return seqlen <= 0 ? 0 : (seqlen + kT - 1) / kT; }
+extern "C" int32_t mc_scan_n_chunks(int32_t seqlen) { return seqlen <= 0 ? 0 : (seqlen + kS - 1) / kS; }
 
 extern "C" size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate) {
   return (size_t)batch * dim * mc_scan_n_chunks(seqlen) * dstate * sizeof(float);
@@ -329,14 +332,15 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_scan_fwd: null params");
   int rc = validate_common(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups, p->itype, p->wtype, "mc_scan_fwd");
   if (rc) return rc;
-  MC_CHECK(p->u && p->delta && p->A && p->B && p->C && p->out, MC_ERR_INVALID,
-           "mc_scan_fwd: u, delta, A, B, C and out must be non-null");
   hipStream_t s = (hipStream_t)stream;
   if (p->batch == 0 || p->seqlen == 0) {
     // nothing to scan; a zero-length sequence leaves the state at zero
-    if (p->last_state) (void)hipMemsetAsync(p->last_state, 0, (size_t)p->batch * p->dim * p->dstate * 4, s);
+    if (p->last_state && p->batch > 0)
+      (void)hipMemsetAsync(p->last_state, 0, (size_t)p->batch * p->dim * p->dstate * 4, s);
     return MC_OK;
   }
+  MC_CHECK(p->u && p->delta && p->A && p->B && p->C && p->out, MC_ERR_INVALID,
+           "mc_scan_fwd: u, delta, A, B, C and out must be non-null");
   const size_t need = bct_bytes(p->batch, p->seqlen, p->dstate, p->n_groups);
   MC_CHECK(p->workspace && p->workspace_bytes >= need && aligned16(p->workspace), MC_ERR_WORKSPACE,
            "mc_scan_fwd: workspace must be >= %zu bytes and 16-B aligned (got %zu)", need, p->workspace_bytes);
@@ -348,7 +352,8 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
 
   FwdArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
-  a.n_chunks = mc_scan_n_chunks(p->seqlen);
+  a.n_chunks = (p->seqlen + kT - 1) / kT;
+  a.n_states = mc_scan_n_chunks(p->seqlen);
   const int H = p->dim / p->n_groups;
   a.nblk = (H + kRows - 1) / kRows;
   a.total_blocks = p->batch * p->n_groups * a.nblk;

@@ -40,10 +40,10 @@ def test_host_only_entry_points():
     lib = _lib.load()
     assert lib.mc_scan_n_chunks(0) == 0
     assert lib.mc_scan_n_chunks(1) == 1
-    assert lib.mc_scan_n_chunks(32) == 1
-    assert lib.mc_scan_n_chunks(33) == 2
-    assert lib.mc_scan_n_chunks(4096) == 128
-    assert lib.mc_scan_chunk_states_bytes(2, 3, 77, 16) == 2 * 3 * 3 * 16 * 4
+    assert lib.mc_scan_n_chunks(16) == 1
+    assert lib.mc_scan_n_chunks(17) == 2
+    assert lib.mc_scan_n_chunks(4096) == 256
+    assert lib.mc_scan_chunk_states_bytes(2, 3, 77, 16) == 2 * 3 * 5 * 16 * 4
 
 
 def test_validation_errors_without_launch():

@@ -13,6 +13,7 @@ ap.add_argument("--shape", default="64,3072,4096,16")
 ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--noz", action="store_true")
+ap.add_argument("--bwd", action="store_true", help="time forward+backward (training) instead")
 args = ap.parse_args()
 Bsz, D, L, N = map(int, args.shape.split(","))
 dt = {"bf16": torch.bfloat16, "f32": torch.float32}[args.dtype]
@@ -26,17 +27,29 @@ Bm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
 Cm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
 Dv = torch.ones(D, device=dev)
 bias = torch.rand(D, device=dev) * 4 - 5
+if args.bwd:
+    for t in (u, delta, A, Bm, Cm, Dv, bias) + ((z,) if z is not None else ()):
+        t.requires_grad_(True)
+    g_out = torch.randn(Bsz, D, L, device=dev, dtype=dt)
+
+
+def step():
+    out = selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
+    if args.bwd:
+        out.backward(g_out)
+
+
 for _ in range(3):
-    selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
+    step()
 torch.cuda.synchronize()
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 s.record()
 for _ in range(args.iters):
-    selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
+    step()
 e.record()
 torch.cuda.synchronize()
 ms = s.elapsed_time(e) / args.iters
 es = u.element_size()
 nbytes = Bsz * D * L * es * (4 if z is not None else 3) + 2 * Bsz * N * L * es + (D * N + 2 * D) * 4
-print(f"shape {args.shape} {args.dtype} z={z is not None}: {ms:.3f} ms  {nbytes / ms / 1e6:.1f} GB/s "
+print(f"shape {args.shape} {args.dtype} z={z is not None} bwd={args.bwd}: {ms:.3f} ms  {nbytes / ms / 1e6:.1f} GB/s "
       f"({nbytes / ms / 1e6 / 8000 * 100:.1f}% of 8 TB/s)")
