@@ -1,0 +1,74 @@
+/*
+ * mc_contrastive.h -- C ABI of the MI355X contrastive-loss kernels (libmamba_clip_amd.so).
+ *
+ * Replaces the dense math of the reference's ClipLoss
+ * (/root/reference/src/mamba_clip/loss.py):
+ *   get_logits     loss.py:89-113   logits = logit_scale * I @ T^T (global, local or single process)
+ *   forward        loss.py:124-147  (CE(logits_img, labels) + CE(logits_txt, labels)) / 2
+ *   get_ground_truth loss.py:76-87  labels = arange(n) (+ n * rank for local_loss)
+ * The feature all-gather (loss.py:16-44) stays in torch.distributed (RCCL)
+ * on the host side; these entry points see plain device pointers.
+ *
+ * Conventions: row-major matrices with a leading dimension in elements; all
+ * statistics and logits fp32; launches are asynchronous on `stream`; the
+ * library never allocates.  Return MC_OK (0) or a negative MC_ERR_* code
+ * (see mc_scan.h) with mc_last_error() describing it.
+ */
+#ifndef MAMBA_CLIP_AMD_MC_CONTRASTIVE_H
+#define MAMBA_CLIP_AMD_MC_CONTRASTIVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mc_scan.h" /* mc_dtype, MC_OK / MC_ERR_* */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* C[m, n] = alpha * sum_k A[m, k] * B[n, k]   (A: M x K, B: N x K, K contiguous)
+ * dtype of A and B: MC_DTYPE_BF16 (MFMA bf16, fp32 accumulate) or
+ * MC_DTYPE_F32 (exact-fp32 MFMA).  alpha = *alpha_dev if alpha_dev != NULL
+ * (a device scalar such as logit_scale.exp(): no host sync), else alpha.
+ * C is fp32 (out_dtype MC_DTYPE_F32) or bf16 (MC_DTYPE_BF16). */
+typedef struct mc_gemm_nt_params {
+  int32_t M, N, K;
+  int32_t in_dtype, out_dtype;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  float alpha;
+  const float* alpha_dev;
+} mc_gemm_nt_params;
+
+int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream);
+
+/* Softmax cross-entropy statistics along the rows (axis = 0: one value per
+ * row, reduce over columns) or the columns (axis = 1) of an fp32 matrix S
+ * (rows x cols, leading dimension lds):
+ *   lse[i]     = log sum_j exp(S[i, j])            (row i; or column i for axis 1)
+ *   nll[i]     = lse[i] - S[i, label_i]            label_i = i + label_offset
+ * loss_out (device scalar, nullable) = sum_i nll[i] * loss_coef. */
+int mc_ce_stats(int32_t rows, int32_t cols, const float* S, int64_t lds, int32_t axis, int64_t label_offset,
+                float* lse, float* nll, float loss_coef, float* loss_out, void* workspace, size_t workspace_bytes,
+                void* stream);
+size_t mc_ce_stats_workspace_bytes(int32_t rows, int32_t cols, int32_t axis);
+
+/* Gradient of  coef_r * sum_i nll_row[i] + coef_c * sum_j nll_col[j]  w.r.t. S,
+ * times the upstream scalar *gout_dev:
+ *   G[i, j] = gout * ( coef_r * (exp(S_ij - lse_r[i]) - [j == i + off_r])
+ *                    + coef_c * (exp(S_ij - lse_c[j]) - [i == j + off_c]) )
+ * (lse_c == NULL drops the column term).  G is written in out_dtype
+ * (fp32 / bf16).  If dscale_out != NULL it also accumulates
+ * sum_ij G_ij * S_ij / scale (scale = *scale_dev): the gradient of the loss
+ * w.r.t. logit_scale, deterministic two-pass reduction in workspace. */
+int mc_ce_grad(int32_t rows, int32_t cols, const float* S, int64_t lds, const float* lse_r, int64_t off_r,
+               float coef_r, const float* lse_c, int64_t off_c, float coef_c, const float* gout_dev,
+               int32_t out_dtype, void* G, int64_t ldg, const float* scale_dev, float* dscale_out, void* workspace,
+               size_t workspace_bytes, void* stream);
+size_t mc_ce_grad_workspace_bytes(int32_t rows, int32_t cols);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAMBA_CLIP_AMD_MC_CONTRASTIVE_H */

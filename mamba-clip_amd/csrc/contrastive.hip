@@ -1,0 +1,414 @@
+// contrastive.hip -- gathered InfoNCE (ClipLoss) math for MI355X (gfx950).
+//
+// Reference: /root/reference/src/mamba_clip/loss.py:89-147 (get_logits + forward):
+//   logits = logit_scale * I @ T^T ;  loss = (CE(logits, arange) + CE(logits^T, arange)) / 2
+// (local_loss: two (b x N) logit blocks against the gathered features, labels
+//  offset by b * rank).  The gather itself is torch.distributed (RCCL).
+//
+// Kernels
+//  * gemm_nt: C = alpha * A B^T on the matrix cores.  128x128 output tile per
+//    256-thread workgroup (4 waves, 64x64 each = 4x4 MFMA tiles), K staged
+//    through LDS in 64-byte row slices (80-byte padded rows: conflict-free
+//    fragment reads), next slice prefetched into registers under the MFMAs.
+//    bf16 inputs use v_mfma_f32_16x16x32_bf16 (fp32 accumulate); fp32 inputs
+//    use the exact-fp32 v_mfma_f32_16x16x4_f32.  alpha may live on the device
+//    (logit_scale.exp()), so the loss needs no host sync.
+//  * ce_rows / ce_cols(+finalize): log-sum-exp statistics and per-label NLL
+//    along rows or columns, online max/sum, deterministic fixed-order
+//    partial reductions (no atomics).
+//  * ce_grad: fused softmax-minus-onehot gradient for the row and column CE
+//    terms in one pass, plus the logit_scale gradient sum(G*S)/scale.
+#include <algorithm>
+
+#include "mc_common.h"
+#include "../../include/mc_contrastive.h"
+
+namespace mc {
+namespace ctr {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BM = 128, BN = 128;
+constexpr int kRowBytes = 64;            // one K slice of a tile row
+constexpr int kLdsStride = 80;           // padded row (bytes): conflict-free 16-lane fragment reads
+constexpr int kTileBytes = BM * kLdsStride;
+
+struct GemmArgs {
+  int M, N, K;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  float alpha; const float* alpha_dev;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <typename TIn, typename TOut, bool kAligned>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
+  constexpr int E = (int)sizeof(TIn);
+  constexpr int BK = kRowBytes / E;       // K elements per slice: 32 (bf16) or 16 (fp32)
+  constexpr int V = 16 / E;               // elements per 16-B vector
+  __shared__ __attribute__((aligned(16))) char lds[4 * kTileBytes];   // A0 B0 A1 B1
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int bid = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const TIn* __restrict__ A = reinterpret_cast<const TIn*>(g.A);
+  const TIn* __restrict__ B = reinterpret_cast<const TIn*>(g.B);
+
+  // each thread moves 2 vectors of A and 2 of B per slice: v = tid + 256*i -> row v/4, chunk v%4
+  uint4 ra[2], rb[2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v >> 2, c = v & 3;
+      const int kk = k0 + c * V;
+      const int am = m0 + r, bn = n0 + r;
+      if (kAligned && kk + V <= g.K) {
+        ra[i] = am < g.M ? ld16(A + (int64_t)am * g.lda + kk) : make_uint4(0u, 0u, 0u, 0u);
+        rb[i] = bn < g.N ? ld16(B + (int64_t)bn * g.ldb + kk) : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        const int nv = max(0, min(V, g.K - kk));
+        ra[i] = am < g.M ? ld16_masked(A + (int64_t)am * g.lda + kk, nv) : make_uint4(0u, 0u, 0u, 0u);
+        rb[i] = bn < g.N ? ld16_masked(B + (int64_t)bn * g.ldb + kk, nv) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* la = lds + (2 * buf) * kTileBytes;
+    char* lb = la + kTileBytes;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v >> 2, c = v & 3;
+      st16(la + r * kLdsStride + c * 16, ra[i]);
+      st16(lb + r * kLdsStride + c * 16, rb[i]);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BK);
+    const char* la = lds + (2 * buf) * kTileBytes;
+    const char* lb = la + kTileBytes;
+    if constexpr (E == 2) {
+      // lane: row (l & 15) of each 16-row tile, k = 8*(l>>4) .. +7 of the 32-wide slice
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *reinterpret_cast<const bf16x8*>(la + (wr * 64 + i * 16 + (lane & 15)) * kLdsStride + (lane >> 4) * 16);
+        bf[i] = *reinterpret_cast<const bf16x8*>(lb + (wc * 64 + i * 16 + (lane & 15)) * kLdsStride + (lane >> 4) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    } else {
+      // exact fp32: 4 MFMA K-steps of 4; lane holds A[row l&15][k = 4s + (l>>4)]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          af[i] = *reinterpret_cast<const float*>(la + (wr * 64 + i * 16 + (lane & 15)) * kLdsStride + (4 * s + (lane >> 4)) * 4);
+          bf[i] = *reinterpret_cast<const float*>(lb + (wc * 64 + i * 16 + (lane & 15)) * kLdsStride + (4 * s + (lane >> 4)) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < nk) {
+      __syncthreads();  // everyone done reading the other buffer (two slices ago)
+      store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
+  TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
+  // C/D map of 16x16 MFMA: col = lane & 15, row = 4*(lane >> 4) + r
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (row < g.M && col < g.N) C[(int64_t)row * g.ldc + col] = from_f<TOut>(alpha * acc[i][j][r]);
+      }
+    }
+}
+
+// ------------------------------------------------------------------ CE statistics
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mm = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+  m = mm;
+}
+
+// one wave per row: lse and nll, per-block partial NLL sums (4 rows per block)
+__global__ __launch_bounds__(256) void ce_rows_kernel(int rows, int cols, const float* __restrict__ S, int64_t lds,
+                                                      int64_t off, float* __restrict__ lse, float* __restrict__ nll,
+                                                      float* __restrict__ partial) {
+  __shared__ float pn[4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + w;
+  float v = 0.f;
+  if (row < rows) {
+    const float* sr = S + (int64_t)row * lds;
+    float m = -INFINITY, s = 0.f;
+    for (int j = lane; j < cols; j += 64) {
+      const float x = sr[j];
+      if (x > m) { s = s * __expf(m - x) + 1.f; m = x; }
+      else s += __expf(x - m);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float m2 = __shfl_xor(m, o), s2 = __shfl_xor(s, o);
+      lse_merge(m, s, m2, s2);
+    }
+    const float l = m + __logf(s);
+    const int64_t lab = row + off;
+    const float tgt = (lab >= 0 && lab < cols) ? sr[lab] : 0.f;
+    v = l - tgt;
+    if (lane == 0) {
+      lse[row] = l;
+      if (nll) nll[row] = v;
+    }
+  }
+  if (lane == 0) pn[w] = row < rows ? v : 0.f;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (pn[0] + pn[1]) + (pn[2] + pn[3]);
+}
+
+// columns: block = 64 columns x 4 row lanes, grid.y = row splits; writes (m, s) partials
+__global__ __launch_bounds__(256) void ce_cols_partial_kernel(int rows, int cols, const float* __restrict__ S,
+                                                              int64_t lds, int splits, float2* __restrict__ part) {
+  __shared__ float2 red[4][64];
+  const int cx = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cx;
+  const int per = (rows + splits - 1) / splits;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float m = -INFINITY, s = 0.f;
+  if (col < cols) {
+    for (int r = r0 + q; r < r1; r += 4) {
+      const float x = S[(int64_t)r * lds + col];
+      if (x > m) { s = s * __expf(m - x) + 1.f; m = x; }
+      else s += __expf(x - m);
+    }
+  }
+  red[q][cx] = make_float2(m, s);
+  __syncthreads();
+  if (q == 0 && col < cols) {
+#pragma unroll
+    for (int k = 1; k < 4; ++k) lse_merge(m, s, red[k][cx].x, red[k][cx].y);
+    part[(int64_t)blockIdx.y * cols + col] = make_float2(m, s);
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_cols_final_kernel(int rows, int cols, const float* __restrict__ S,
+                                                            int64_t lds, int splits, const float2* __restrict__ part,
+                                                            int64_t off, float* __restrict__ lse,
+                                                            float* __restrict__ nll, float* __restrict__ partial) {
+  __shared__ float pn[256];
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  float v = 0.f;
+  if (col < cols) {
+    float m = -INFINITY, s = 0.f;
+    for (int k = 0; k < splits; ++k) {
+      const float2 p = part[(int64_t)k * cols + col];
+      lse_merge(m, s, p.x, p.y);
+    }
+    const float l = m + __logf(s);
+    const int64_t lab = col + off;
+    const float tgt = (lab >= 0 && lab < rows) ? S[lab * lds + col] : 0.f;
+    v = l - tgt;
+    lse[col] = l;
+    if (nll) nll[col] = v;
+  }
+  pn[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) pn[threadIdx.x] += pn[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = pn[0];
+}
+
+// fixed-order sum of n partials -> out[0] = coef * sum  (one block)
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int n, float coef,
+                                                           const float* __restrict__ divisor, float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = coef * red[0] / (divisor ? *divisor : 1.f);
+}
+
+// G = gout * (coef_r (softmax_r - onehot_r) + coef_c (softmax_c - onehot_c)); partial sum(G * S)
+template <typename TOut>
+__global__ __launch_bounds__(256) void ce_grad_kernel(int rows, int cols, const float* __restrict__ S, int64_t lds,
+                                                      const float* __restrict__ lse_r, int64_t off_r, float coef_r,
+                                                      const float* __restrict__ lse_c, int64_t off_c, float coef_c,
+                                                      const float* __restrict__ gout_dev, TOut* __restrict__ G,
+                                                      int64_t ldg, float* __restrict__ partial) {
+  __shared__ float red[256];
+  const float gout = gout_dev ? *gout_dev : 1.f;
+  const int64_t total = (int64_t)rows * cols;
+  float acc = 0.f;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int i = (int)(idx / cols), j = (int)(idx % cols);
+    const float s = S[(int64_t)i * lds + j];
+    float gv = coef_r * (__expf(s - lse_r[i]) - ((int64_t)j == i + off_r ? 1.f : 0.f));
+    if (lse_c) gv += coef_c * (__expf(s - lse_c[j]) - ((int64_t)i == j + off_c ? 1.f : 0.f));
+    gv *= gout;
+    G[(int64_t)i * ldg + j] = from_f<TOut>(gv);
+    acc = fmaf(gv, s, acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && partial) partial[blockIdx.x] = red[0];
+}
+
+constexpr int kColSplits = 32;
+constexpr int kGradGrid = 2048;
+
+}  // namespace ctr
+}  // namespace mc
+
+using namespace mc;
+using namespace mc::ctr;
+
+extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_gemm_nt: null params");
+  MC_CHECK(p->M >= 0 && p->N >= 0 && p->K >= 0, MC_ERR_SHAPE, "mc_gemm_nt: negative shape");
+  MC_CHECK(p->in_dtype == MC_DTYPE_BF16 || p->in_dtype == MC_DTYPE_F32, MC_ERR_DTYPE,
+           "mc_gemm_nt: inputs must be bf16 or fp32");
+  MC_CHECK(p->out_dtype == MC_DTYPE_F32 || p->out_dtype == MC_DTYPE_BF16, MC_ERR_DTYPE,
+           "mc_gemm_nt: output must be fp32 or bf16");
+  if (p->M == 0 || p->N == 0) return MC_OK;
+  MC_CHECK(p->A && p->B && p->C, MC_ERR_INVALID, "mc_gemm_nt: null operand");
+  GemmArgs g;
+  g.M = p->M; g.N = p->N; g.K = p->K;
+  g.A = p->A; g.lda = p->lda; g.B = p->B; g.ldb = p->ldb; g.C = p->C; g.ldc = p->ldc;
+  g.alpha = p->alpha; g.alpha_dev = p->alpha_dev;
+  g.tiles_m = (p->M + BM - 1) / BM;
+  g.tiles_n = (p->N + BN - 1) / BN;
+  const int eb = p->in_dtype == MC_DTYPE_F32 ? 4 : 2;
+  const int64_t v = 16 / eb;
+  const bool aligned = aligned16(p->A) && aligned16(p->B) && p->lda % v == 0 && p->ldb % v == 0;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(g.tiles_m * g.tiles_n), block(256);
+#define MC_GEMM(TI, TO)                                                                   \
+  do {                                                                                    \
+    if (aligned) hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, true>), grid, block, 0, s, g); \
+    else hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, false>), grid, block, 0, s, g);       \
+  } while (0)
+  if (p->in_dtype == MC_DTYPE_BF16) {
+    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(bf16_t, float); else MC_GEMM(bf16_t, bf16_t);
+  } else {
+    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(float, float); else MC_GEMM(float, bf16_t);
+  }
+#undef MC_GEMM
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_nt: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+extern "C" size_t mc_ce_stats_workspace_bytes(int32_t rows, int32_t cols, int32_t axis) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (axis == 0) return (size_t)((rows + 3) / 4) * sizeof(float);
+  return (size_t)kColSplits * cols * sizeof(float2) + (size_t)((cols + 255) / 256) * sizeof(float) + 256;
+}
+
+extern "C" int mc_ce_stats(int32_t rows, int32_t cols, const float* S, int64_t lds, int32_t axis,
+                           int64_t label_offset, float* lse, float* nll, float loss_coef, float* loss_out,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  MC_CHECK(rows > 0 && cols > 0, MC_ERR_SHAPE, "mc_ce_stats: empty matrix");
+  MC_CHECK(axis == 0 || axis == 1, MC_ERR_INVALID, "mc_ce_stats: axis must be 0 (rows) or 1 (columns)");
+  MC_CHECK(S && lse, MC_ERR_INVALID, "mc_ce_stats: null S / lse");
+  const size_t need = mc_ce_stats_workspace_bytes(rows, cols, axis);
+  MC_CHECK(workspace && workspace_bytes >= need && aligned16(workspace), MC_ERR_WORKSPACE,
+           "mc_ce_stats: workspace must be >= %zu bytes, 16-B aligned", need);
+  hipStream_t s = (hipStream_t)stream;
+  if (axis == 0) {
+    const int nb = (rows + 3) / 4;
+    float* part = reinterpret_cast<float*>(workspace);
+    hipLaunchKernelGGL(ce_rows_kernel, dim3(nb), dim3(256), 0, s, rows, cols, S, lds, label_offset, lse, nll, part);
+    if (loss_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, nb, loss_coef, nullptr, loss_out);
+  } else {
+    float2* part = reinterpret_cast<float2*>(workspace);
+    float* lpart = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + (size_t)kColSplits * cols * sizeof(float2));
+    const int splits = std::min(kColSplits, rows);
+    hipLaunchKernelGGL(ce_cols_partial_kernel, dim3((cols + 63) / 64, splits), dim3(256), 0, s, rows, cols, S, lds,
+                       splits, part);
+    const int nb = (cols + 255) / 256;
+    hipLaunchKernelGGL(ce_cols_final_kernel, dim3(nb), dim3(256), 0, s, rows, cols, S, lds, splits, part,
+                       label_offset, lse, nll, lpart);
+    if (loss_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, lpart, nb, loss_coef, nullptr, loss_out);
+  }
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_ce_stats: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+extern "C" size_t mc_ce_grad_workspace_bytes(int32_t rows, int32_t cols) {
+  (void)rows; (void)cols;
+  return (size_t)kGradGrid * sizeof(float);
+}
+
+extern "C" int mc_ce_grad(int32_t rows, int32_t cols, const float* S, int64_t lds, const float* lse_r, int64_t off_r,
+                          float coef_r, const float* lse_c, int64_t off_c, float coef_c, const float* gout_dev,
+                          int32_t out_dtype, void* G, int64_t ldg, const float* scale_dev, float* dscale_out,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  MC_CHECK(rows > 0 && cols > 0, MC_ERR_SHAPE, "mc_ce_grad: empty matrix");
+  MC_CHECK(S && lse_r && G, MC_ERR_INVALID, "mc_ce_grad: null S / lse_r / G");
+  MC_CHECK(out_dtype == MC_DTYPE_F32 || out_dtype == MC_DTYPE_BF16, MC_ERR_DTYPE, "mc_ce_grad: G must be fp32/bf16");
+  MC_CHECK(!dscale_out || (workspace && workspace_bytes >= mc_ce_grad_workspace_bytes(rows, cols)), MC_ERR_WORKSPACE,
+           "mc_ce_grad: workspace too small for the logit_scale gradient");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = (int64_t)rows * cols;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, kGradGrid);
+  float* part = dscale_out ? reinterpret_cast<float*>(workspace) : nullptr;
+  if (out_dtype == MC_DTYPE_F32)
+    hipLaunchKernelGGL((ce_grad_kernel<float>), dim3(grid), dim3(256), 0, s, rows, cols, S, lds, lse_r, off_r, coef_r,
+                       lse_c, off_c, coef_c, gout_dev, reinterpret_cast<float*>(G), ldg, part);
+  else
+    hipLaunchKernelGGL((ce_grad_kernel<bf16_t>), dim3(grid), dim3(256), 0, s, rows, cols, S, lds, lse_r, off_r,
+                       coef_r, lse_c, off_c, coef_c, gout_dev, reinterpret_cast<bf16_t*>(G), ldg, part);
+  if (dscale_out)
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, grid, 1.f, scale_dev, dscale_out);
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_ce_grad: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}

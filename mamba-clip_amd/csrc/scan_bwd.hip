@@ -377,28 +377,28 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
   }
 }
 
-template <int kN>
-__global__ __launch_bounds__(256) void scan_bwd_reduce_params(const float* __restrict__ slab_a,
-                                                               const float* __restrict__ slab_d,
-                                                               const float* __restrict__ slab_bias, int batch, int dim,
-                                                               int dstate, float* __restrict__ dA, float* __restrict__ dD,
-                                                               float* __restrict__ dbias) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < dim * dstate) {
-    const int d = i / dstate, n = i % dstate;
-    float s = 0.f;
-    for (int bb = 0; bb < batch; ++bb) s += slab_a[((int64_t)bb * dim + d) * kN + n];
-    dA[i] = s;
+// Column sums over the batch: out[c] = sum_b in[b][c] (row stride ld).  A
+// block = 32 columns x 8 batch lanes; the 8 partials meet in LDS in a fixed
+// order (deterministic).  Used for dA (cols = (d, n)), dD and dbias (cols = d).
+__global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__ in, int batch, int cols, int64_t ld,
+                                                       int out_cols, int col_div, int col_mod, float* __restrict__ out) {
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  float s = 0.f;
+  if (c < cols)
+    for (int bb = q; bb < batch; bb += 8) s += in[(int64_t)bb * ld + c];
+  part[q][cx] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][cx];
+    // column c of the slab -> output index (drop padded states: c = d*col_div + n, keep n < col_mod)
+    const int d = c / col_div, n = c % col_div;
+    if (n < col_mod) out[(int64_t)d * col_mod + n] = t;
   }
-  if (i < dim) {
-    float sd = 0.f, sb = 0.f;
-    for (int bb = 0; bb < batch; ++bb) {
-      sd += slab_d[(int64_t)bb * dim + i];
-      sb += slab_bias[(int64_t)bb * dim + i];
-    }
-    if (dD) dD[i] = sd;
-    if (dbias) dbias[i] = sb;
-  }
+  (void)out_cols;
 }
 
 struct BwdWs {
@@ -445,9 +445,15 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL((scan_bwd_reduce_bc<TW, kN>), dim3(grid), dim3(256), 0, s, a.slab_bc, a.batch, a.n_groups,
                      a.nblk, a.dstate, a.seqlen, reinterpret_cast<TW*>(dB), reinterpret_cast<TW*>(dC));
-  const int n = std::max(a.dim * a.dstate, a.dim);
-  hipLaunchKernelGGL((scan_bwd_reduce_params<kN>), dim3((n + 255) / 256), dim3(256), 0, s, a.slab_a, a.slab_d,
-                     a.slab_bias, a.batch, a.dim, a.dstate, dA, dD, dbias);
+  const int ca = a.dim * kN;
+  hipLaunchKernelGGL(scan_bwd_colsum, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, ca, (int64_t)ca,
+                     a.dim * a.dstate, kN, a.dstate, dA);
+  if (dD)
+    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_d, a.batch, a.dim,
+                       (int64_t)a.dim, a.dim, 1, 1, dD);
+  if (dbias)
+    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_bias, a.batch, a.dim,
+                       (int64_t)a.dim, a.dim, 1, 1, dbias);
 }
 
 template <typename TW>

@@ -55,6 +55,15 @@ class ScanBwdParams(ctypes.Structure):
     ]
 
 
+class GemmNTParams(ctypes.Structure):
+    """Mirror of ``mc_gemm_nt_params`` (include/mc_contrastive.h)."""
+    _fields_ = [
+        ("M", c_i32), ("N", c_i32), ("K", c_i32), ("in_dtype", c_i32), ("out_dtype", c_i32),
+        ("A", c_vp), ("lda", c_i64), ("B", c_vp), ("ldb", c_i64), ("C", c_vp), ("ldc", c_i64),
+        ("alpha", ctypes.c_float), ("alpha_dev", c_fp),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -65,6 +74,13 @@ SYMBOLS = {
     "mc_scan_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd": (ctypes.c_int, [ctypes.POINTER(ScanFwdParams), c_vp]),
     "mc_scan_bwd": (ctypes.c_int, [ctypes.POINTER(ScanBwdParams), c_vp]),
+    "mc_gemm_nt": (ctypes.c_int, [ctypes.POINTER(GemmNTParams), c_vp]),
+    "mc_ce_stats": (ctypes.c_int, [c_i32, c_i32, c_fp, c_i64, c_i32, c_i64, c_fp, c_fp, ctypes.c_float, c_fp,
+                                   c_vp, ctypes.c_size_t, c_vp]),
+    "mc_ce_stats_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+    "mc_ce_grad": (ctypes.c_int, [c_i32, c_i32, c_fp, c_i64, c_fp, c_i64, ctypes.c_float, c_fp, c_i64,
+                                  ctypes.c_float, c_fp, c_i32, c_vp, c_i64, c_fp, c_fp, c_vp, ctypes.c_size_t, c_vp]),
+    "mc_ce_grad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
 }
 
 _lib = None

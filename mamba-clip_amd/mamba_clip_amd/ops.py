@@ -1,0 +1,114 @@
+"""Thin torch-facing wrappers of the contrastive kernels (include/mc_contrastive.h).
+
+``gemm_nt(A, B, alpha)``  C = alpha * A @ B.T on the matrix cores (bf16 or fp32 in).
+``scaled_logits_ce``      autograd op: logits = scale * X @ Y.T, then a weighted
+                          sum of row- and/or column-softmax cross-entropies --
+                          the dense part of ClipLoss (loss.py:89-147).
+All launches go on the current HIP stream; nothing synchronises.
+"""
+import torch
+
+from . import _lib
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32):
+    """C[m, n] = alpha * sum_k A[m, k] * B[n, k]  (A, B row-major, K contiguous)."""
+    lib = _lib.load()
+    if A.dtype != B.dtype or A.dtype not in (torch.bfloat16, torch.float32):
+        raise RuntimeError("gemm_nt: A and B must both be bf16 or both fp32")
+    if A.stride(-1) != 1:
+        A = A.contiguous()
+    if B.stride(-1) != 1:
+        B = B.contiguous()
+    M, K = A.shape
+    N, K2 = B.shape
+    if K != K2:
+        raise RuntimeError("gemm_nt: inner dimensions differ")
+    C = torch.empty(M, N, device=A.device, dtype=out_dtype)
+    p = _lib.GemmNTParams()
+    p.M, p.N, p.K = M, N, K
+    p.in_dtype, p.out_dtype = _lib.dtype_code(A.dtype), _lib.dtype_code(out_dtype)
+    p.A, p.lda, p.B, p.ldb, p.C, p.ldc = A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), N
+    p.alpha = float(alpha)
+    p.alpha_dev = alpha_dev.data_ptr() if alpha_dev is not None else None
+    _lib.check(lib.mc_gemm_nt(p, _lib.stream_handle(A.device)), "mc_gemm_nt")
+    return C
+
+
+def ce_stats(S, axis, label_offset, coef):
+    """(lse, weighted NLL sum as a device scalar) along rows (axis 0) or columns (1)."""
+    lib = _lib.load()
+    rows, cols = S.shape
+    n = rows if axis == 0 else cols
+    lse = torch.empty(n, device=S.device, dtype=torch.float32)
+    loss = torch.empty((), device=S.device, dtype=torch.float32)
+    ws_b = lib.mc_ce_stats_workspace_bytes(rows, cols, axis)
+    ws = _ws(ws_b, S.device)
+    _lib.check(lib.mc_ce_stats(rows, cols, S.data_ptr(), S.stride(0), axis, int(label_offset), lse.data_ptr(),
+                               None, float(coef), loss.data_ptr(), ws.data_ptr(), ws_b,
+                               _lib.stream_handle(S.device)), "mc_ce_stats")
+    return lse, loss
+
+
+def ce_grad(S, lse_r, off_r, coef_r, lse_c, off_c, coef_c, gout, out_dtype, scale):
+    """G = gout * d(loss)/dS (fp32 or bf16) and d(loss)/d(scale) (device scalar)."""
+    lib = _lib.load()
+    rows, cols = S.shape
+    G = torch.empty(rows, cols, device=S.device, dtype=out_dtype)
+    dscale = torch.empty((), device=S.device, dtype=torch.float32)
+    ws_b = lib.mc_ce_grad_workspace_bytes(rows, cols)
+    ws = _ws(ws_b, S.device)
+    gout = gout.reshape(()).float().contiguous()
+    _lib.check(lib.mc_ce_grad(rows, cols, S.data_ptr(), S.stride(0), lse_r.data_ptr(), int(off_r), float(coef_r),
+                              lse_c.data_ptr() if lse_c is not None else None, int(off_c), float(coef_c),
+                              gout.data_ptr(), _lib.dtype_code(out_dtype), G.data_ptr(), cols, scale.data_ptr(),
+                              dscale.data_ptr(), ws.data_ptr(), ws_b, _lib.stream_handle(S.device)), "mc_ce_grad")
+    return G, dscale
+
+
+class ScaledLogitsCE(torch.autograd.Function):
+    """loss = coef_r * sum_i CE_row_i(S) + coef_c * sum_j CE_col_j(S),  S = scale * X @ Y^T.
+
+    Row i's label is column i + row_off; column j's label is row j + col_off.
+    coef_c == 0 drops the column term (local-loss halves).  X and Y are the
+    (gathered) feature matrices; bf16 inputs run the bf16 MFMA path, fp32
+    inputs the exact-fp32 MFMA path; logits and statistics are fp32.
+    """
+
+    @staticmethod
+    def forward(ctx, X, Y, scale, row_off, coef_r, col_off, coef_c):
+        dt = X.dtype if X.dtype in (torch.bfloat16, torch.float32) else torch.float32
+        Xc = X.to(dt).contiguous()
+        Yc = Y.to(dt).contiguous()
+        sc = scale.reshape(()).float().contiguous()
+        S = gemm_nt(Xc, Yc, alpha_dev=sc)
+        lse_r, loss = ce_stats(S, 0, row_off, coef_r)
+        lse_c = None
+        if coef_c != 0.0:
+            lse_c, loss_c = ce_stats(S, 1, col_off, coef_c)
+            loss = loss + loss_c
+        ctx.save_for_backward(Xc, Yc, sc, S, lse_r, lse_c if lse_c is not None else lse_r)
+        ctx.cfg = (row_off, coef_r, col_off, coef_c, lse_c is not None, X.dtype, Y.dtype, scale.dtype, scale.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        Xc, Yc, sc, S, lse_r, lse_c = ctx.saved_tensors
+        row_off, coef_r, col_off, coef_c, has_c, xdt, ydt, sdt, sshape = ctx.cfg
+        gdt = Xc.dtype  # G feeds the MFMA GEMMs in the operands' dtype
+        G, dscale = ce_grad(S, lse_r, row_off, coef_r, lse_c if has_c else None, col_off, coef_c, gout, gdt, sc)
+        dX = dY = None
+        if ctx.needs_input_grad[0]:
+            dX = gemm_nt(G, Yc.t().contiguous(), alpha_dev=sc).to(xdt)           # scale * G @ Y
+        if ctx.needs_input_grad[1]:
+            dY = gemm_nt(G.t().contiguous(), Xc.t().contiguous(), alpha_dev=sc).to(ydt)  # scale * G^T @ X
+        dS = dscale.to(sdt).reshape(sshape) if ctx.needs_input_grad[2] else None
+        return dX, dY, dS, None, None, None, None
+
+
+def scaled_logits_ce(X, Y, scale, row_off=0, coef_r=1.0, col_off=0, coef_c=0.0):
+    return ScaledLogitsCE.apply(X, Y, scale, row_off, coef_r, col_off, coef_c)
