@@ -35,9 +35,10 @@ def create_loss(args):
 def _gather_stacked(image_features, text_features, world_size):
     """One all_gather of the stacked (2, b, E) features (no autograd)."""
     b = image_features.shape[0]
-    stacked = torch.stack([image_features.detach(), text_features.detach()]).contiguous()
-    out = torch.empty((world_size,) + tuple(stacked.shape), device=stacked.device, dtype=stacked.dtype)
-    dist.all_gather_into_tensor(out, stacked)
+    stacked = torch.stack([image_features.detach(), text_features.detach()]).contiguous()   # (2, b, E)
+    out = torch.empty((world_size * 2,) + tuple(stacked.shape[1:]), device=stacked.device, dtype=stacked.dtype)
+    dist.all_gather_into_tensor(out, stacked)          # concatenated along dim 0: rank-major
+    out = out.view(world_size, 2, b, -1)
     imgs = out[:, 0].reshape(world_size * b, -1)
     txts = out[:, 1].reshape(world_size * b, -1)
     return imgs, txts

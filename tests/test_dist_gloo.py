@@ -1,0 +1,85 @@
+"""Multi-process (gloo, CPU) checks of the distributed ClipLoss host logic:
+feature gather (one stacked all_gather), local-slice re-insertion, local_loss
+label offsets and loss coefficients, gather_with_grad -- against the golden
+vectors produced by the reference loss.py under gloo (tests/golden).
+
+The HIP kernels cannot run on CPU, so here the dense op `scaled_logits_ce`
+is replaced by a CPU restatement (the oracle acts as the checker); the same
+op is checked against the oracle on the GPU in test_loss_gpu.py."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT, load_golden
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cpu_scaled_logits_ce(X, Y, scale, row_off=0, coef_r=1.0, col_off=0, coef_c=0.0):
+    S = scale * X @ Y.T
+    r = torch.arange(S.shape[0])
+    loss = coef_r * (torch.logsumexp(S, 1) - S[r, r + row_off]).sum()
+    if coef_c:
+        c = torch.arange(S.shape[1])
+        loss = loss + coef_c * (torch.logsumexp(S, 0) - S[c + col_off, c]).sum()
+    return loss
+
+
+def _worker(rank, world, port, q):
+    try:
+        _worker_body(rank, world, port, q)
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, {"error": repr(e)}))
+
+
+def _worker_body(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+    import torch.distributed as dist
+    import mamba_clip_amd.loss as L
+    L.scaled_logits_ce = _cpu_scaled_logits_ce
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_golden(f"clip_loss_gloo_w{world}.safetensors")
+    b = g["img"].shape[0] // world
+    res = {}
+    for ll in (False, True):
+        for gg in (False, True):
+            img = g["img"][rank * b:(rank + 1) * b].clone().requires_grad_(True)
+            txt = g["txt"][rank * b:(rank + 1) * b].clone().requires_grad_(True)
+            scale = torch.tensor(10.0, requires_grad=True)
+            crit = L.ClipLoss(local_loss=ll, gather_with_grad=gg, cache_labels=True, rank=rank, world_size=world)
+            loss = crit(img, txt, scale)["contrastive_loss"]
+            loss.backward()
+            key = f"ll{int(ll)}_gg{int(gg)}"
+            ok = (torch.allclose(loss.detach().reshape(1), g[f"r{rank}.{key}.loss"], rtol=1e-5, atol=1e-6)
+                  and torch.allclose(img.grad, g[f"r{rank}.{key}.grad_img"], rtol=1e-4, atol=1e-6)
+                  and torch.allclose(txt.grad, g[f"r{rank}.{key}.grad_txt"], rtol=1e-4, atol=1e-6)
+                  and torch.allclose(scale.grad.reshape(1), g[f"r{rank}.{key}.grad_scale"], rtol=1e-4, atol=1e-6))
+            res[key] = bool(ok)
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_clip_loss_distributed_matches_reference(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, res in results.items():
+        assert all(res.values()), f"rank {rank}: {res}"
