@@ -1,0 +1,66 @@
+/*
+ * mc_ops.h -- C ABI of the MI355X encoder kernels around the scan (libmamba_clip_amd.so).
+ *
+ * The reference gets these from third-party packages it imports but does not
+ * vendor (open_clip/timm for the ViT tower, mamba_ssm/causal_conv1d for a
+ * Mamba block: SURVEY.md section 2.2); the build owns them:
+ *   mc_add_rmsnorm_fwd/bwd  fused residual-add + RMSNorm (Mamba block pre-norm,
+ *                           residual stream kept in fp32)
+ *   mc_causal_conv1d_fwd/bwd depthwise causal conv1d (+ optional SiLU) over the
+ *                           sequence of (batch, dim, seqlen) activations, the
+ *                           short conv in front of the scan (the 2-D analogue is
+ *                           SS2D's depthwise conv, model.py:331-339)
+ *   mc_patch_im2col          ViT / VSSM patch-embed input reshuffle: stride ==
+ *                           kernel conv as a GEMM (model.py:189-191 PatchEmbed2D)
+ * Same conventions as mc_scan.h: device pointers, caller-owned buffers,
+ * asynchronous on `stream`, MC_OK / MC_ERR_* return codes.
+ */
+#ifndef MAMBA_CLIP_AMD_MC_OPS_H
+#define MAMBA_CLIP_AMD_MC_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mc_scan.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* h = x + res_in (res_in nullable);  y = h * rsqrt(mean(h^2) + eps) * w
+ * x, y: rows x cols in `dtype` (bf16 / f16 / f32); res_in, res_out, w, rstd fp32.
+ * res_out (rows x cols fp32) receives h; rstd (rows) the inverse RMS. */
+int mc_add_rmsnorm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, const float* res_in, const float* w,
+                       float eps, void* y, float* res_out, float* rstd, void* stream);
+
+/* Backward of the above given dy (dtype) and dres (fp32 gradient of res_out,
+ * nullable): dh = rstd * (w dy - h rstd^2 mean(h w dy)) + dres, written to
+ * dx (dtype, nullable) and dres_in (fp32, nullable); dw (cols, fp32) =
+ * sum_rows dy h rstd, reduced deterministically through the workspace. */
+int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const float* dres, const float* h,
+                       const float* w, const float* rstd, void* dx, float* dres_in, float* dw, void* workspace,
+                       size_t workspace_bytes, void* stream);
+size_t mc_add_rmsnorm_bwd_workspace_bytes(int32_t rows, int32_t cols);
+
+/* y[b, d, t] = act( bias[d] + sum_k w[d, k] * x[b, d, t - (K-1) + k] ), zero left padding.
+ * x: (batch, dim, seqlen) with strides (x_bs, x_ds, 1); y contiguous; w (dim, K) fp32,
+ * bias (dim,) fp32 nullable; act = SiLU if silu else identity.  K <= 8. */
+int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype, const void* x,
+                         int64_t x_bs, int64_t x_ds, const float* w, const float* bias, int32_t silu, void* y,
+                         void* stream);
+
+/* Backward: dx (contiguous, dtype), dw (dim, K) fp32, dbias (dim) fp32 (nullable). */
+int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype, const void* x,
+                         int64_t x_bs, int64_t x_ds, const float* w, const float* bias, int32_t silu, const void* dy,
+                         void* dx, float* dw, float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t K);
+
+/* patches[(b*ph + i)*pw + j, (c*P + ky)*P + kx] = img[b, c, i*P + ky, j*P + kx]
+ * img (batch, C, H, W) contiguous; H % P == W % P == 0; same dtype in and out. */
+int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, int32_t P, int32_t dtype, const void* img,
+                    void* patches, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAMBA_CLIP_AMD_MC_OPS_H */

@@ -1,0 +1,400 @@
+// ops.hip -- encoder kernels around the scan for MI355X (gfx950): fused
+// residual-add + RMSNorm, causal depthwise conv1d (+SiLU), patch im2col.
+// All three are HBM-bound streaming ops: 16-B vector accesses along the
+// contiguous dimension, one pass over the data, fp32 math, deterministic
+// reductions (per-wave partial slabs + fixed-order column sums).
+#include <algorithm>
+
+#include "mc_common.h"
+#include "../../include/mc_ops.h"
+
+namespace mc {
+namespace ops {
+
+// ------------------------------------------------------------------ RMSNorm
+// One wave per row; the row lives in registers between the two passes
+// (cols <= kMaxCols).  Grid-stride over rows so the backward's per-wave dw
+// partials stay few (one slab row per wave).
+constexpr int kMaxVec = 8;  // 16-B vectors per lane per row: cols <= 4096 (16-bit) / 2048 (fp32)
+
+template <typename T>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols, const T* __restrict__ x,
+                                                              const float* __restrict__ res_in,
+                                                              const float* __restrict__ w, float eps,
+                                                              T* __restrict__ y, float* __restrict__ res_out,
+                                                              float* __restrict__ rstd) {
+  constexpr int V = ElemTraits<T>::kVec;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int nvec = cols / V;
+  for (int row = wave; row < rows; row += nwaves) {
+    float h[kMaxVec][V];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        const uint4 q = ld16(x + (int64_t)row * cols + v * V);
+#pragma unroll
+        for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(q, e);
+        if (res_in) {
+          const float* r = res_in + (int64_t)row * cols + v * V;
+#pragma unroll
+          for (int e4 = 0; e4 < V; e4 += 4) {
+            const float4 rq = *reinterpret_cast<const float4*>(r + e4);
+            h[i][e4] += rq.x; h[i][e4 + 1] += rq.y; h[i][e4 + 2] += rq.z; h[i][e4 + 3] += rq.w;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) ss = fmaf(h[i][e], h[i][e], ss);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    const float rs = rsqrtf(ss / cols + eps);
+    if (lane == 0) rstd[row] = rs;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        float o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = h[i][e] * rs * w[v * V + e];
+        st16(y + (int64_t)row * cols + v * V, pack_f<T>(o));
+        if (res_out) {
+          float* r = res_out + (int64_t)row * cols + v * V;
+#pragma unroll
+          for (int e4 = 0; e4 < V; e4 += 4)
+            *reinterpret_cast<float4*>(r + e4) = make_float4(h[i][e4], h[i][e4 + 1], h[i][e4 + 2], h[i][e4 + 3]);
+        }
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
+                                                              const float* __restrict__ dres,
+                                                              const float* __restrict__ hbuf,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ rstd, T* __restrict__ dx,
+                                                              float* __restrict__ dres_in,
+                                                              float* __restrict__ dw_part) {
+  constexpr int V = ElemTraits<T>::kVec;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int nvec = cols / V;
+  float dwacc[kMaxVec][V];
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i)
+#pragma unroll
+    for (int e = 0; e < V; ++e) dwacc[i][e] = 0.f;
+  for (int row = wave; row < rows; row += nwaves) {
+    const float rs = rstd[row];
+    float h[kMaxVec][V], g[kMaxVec][V];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        const uint4 q = ld16(dy + (int64_t)row * cols + v * V);
+        const float* hp = hbuf + (int64_t)row * cols + v * V;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          h[i][e] = hp[e];
+          const float d = elem_f<T>(q, e);
+          g[i][e] = d * w[v * V + e];
+          dot = fmaf(g[i][e], h[i][e], dot);
+          dwacc[i][e] = fmaf(d, h[i][e] * rs, dwacc[i][e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dot += __shfl_xor(dot, o);
+    const float c = dot * rs * rs / cols;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        float o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          o[e] = rs * (g[i][e] - h[i][e] * c);
+          if (dres) o[e] += dres[(int64_t)row * cols + v * V + e];
+        }
+        if (dx) st16(dx + (int64_t)row * cols + v * V, pack_f<T>(o));
+        if (dres_in) {
+          float* r = dres_in + (int64_t)row * cols + v * V;
+#pragma unroll
+          for (int e4 = 0; e4 < V; e4 += 4)
+            *reinterpret_cast<float4*>(r + e4) = make_float4(o[e4], o[e4 + 1], o[e4 + 2], o[e4 + 3]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int v = lane + 64 * i;
+    if (v < nvec)
+#pragma unroll
+      for (int e = 0; e < V; ++e) dw_part[(int64_t)wave * cols + v * V + e] = dwacc[i][e];
+  }
+}
+
+// out[c] = sum_r in[r][c]: 32 columns x 8 row lanes per block, fixed order
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ in, int nrows, int cols,
+                                                     float* __restrict__ out) {
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  float s = 0.f;
+  if (c < cols)
+    for (int r = q; r < nrows; r += 8) s += in[(int64_t)r * cols + c];
+  part[q][cx] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][cx];
+    out[c] = t;
+  }
+}
+
+constexpr int kNormGrid = 256;  // blocks of 4 waves: 1024 waves -> 1024 dw partial rows
+
+// ------------------------------------------------------------------ causal conv1d
+// One thread per (b, d) row: sliding window over the sequence in registers;
+// per-row dw/dbias partials in the backward.
+constexpr int kMaxK = 8;
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+                                                         int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int silu,
+                                                         T* __restrict__ y) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= (int64_t)batch * dim) return;
+  const int b = (int)(row / dim), d = (int)(row % dim);
+  const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
+  T* yr = y + row * L;
+  float wk[kMaxK], win[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) { wk[k] = k < K ? w[d * K + k] : 0.f; win[k] = 0.f; }
+  const float bv = bias ? bias[d] : 0.f;
+  for (int t = 0; t < L; ++t) {
+#pragma unroll
+    for (int k = 0; k < kMaxK - 1; ++k) win[k] = win[k + 1];
+    win[kMaxK - 1] = to_f(xr[t]);
+    float acc = bv;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K) acc = fmaf(wk[k], win[kMaxK - K + k], acc);
+    yr[t] = from_f<T>(silu ? silu_f(acc) : acc);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+                                                         int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int silu,
+                                                         const T* __restrict__ dy, T* __restrict__ dx,
+                                                         float* __restrict__ part) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= (int64_t)batch * dim) return;
+  const int b = (int)(row / dim), d = (int)(row % dim);
+  const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
+  const T* gr = dy + row * L;
+  T* dxr = dx + row * L;
+  float wk[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
+  const float bv = bias ? bias[d] : 0.f;
+  // reverse walk: dpre window holds dpre[t .. t+K-1]; x window x[t-K+1 .. t]
+  float dwk[kMaxK], db = 0.f, dp[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) { dwk[k] = 0.f; dp[k] = 0.f; }
+  for (int t = L - 1; t >= 0; --t) {
+    // pre-activation at t (recomputed) and its gradient
+    float xw[kMaxK];
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+      const int tt = t - (K - 1) + k;
+      xw[k] = (k < K && tt >= 0) ? to_f(xr[tt]) : 0.f;
+    }
+    float pre = bv;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K) pre = fmaf(wk[k], xw[k], pre);
+    float g = to_f(gr[t]);
+    if (silu) {
+      const float s = sigmoid_f(pre);
+      g *= s * (1.f + pre * (1.f - s));
+    }
+    // shift: dp[k] = dpre[t + k]
+#pragma unroll
+    for (int k = kMaxK - 1; k > 0; --k) dp[k] = dp[k - 1];
+    dp[0] = g;
+    db += g;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K) dwk[k] = fmaf(g, xw[k], dwk[k]);
+    // dx[t] = sum_k w[k] * dpre[t + (K-1) - k]
+    float gx = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K && t + (K - 1) - k < L) gx = fmaf(wk[k], dp[K - 1 - k], gx);
+    dxr[t] = from_f<T>(gx);
+  }
+  float* pr = part + row * (kMaxK + 1);
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) pr[k] = dwk[k];
+  pr[kMaxK] = db;
+}
+
+// dw[d, k] = sum_b part[b, d, k]; dbias[d] = sum_b part[b, d, K]
+__global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restrict__ part, int batch, int dim, int K,
+                                                            float* __restrict__ dw, float* __restrict__ dbias) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dim * (K + 1)) return;
+  const int d = i / (K + 1), k = i % (K + 1);
+  const int slot = k < K ? k : kMaxK;
+  float s = 0.f;
+  for (int b = 0; b < batch; ++b) s += part[((int64_t)b * dim + d) * (kMaxK + 1) + slot];
+  if (k < K) dw[d * K + k] = s;
+  else if (dbias) dbias[d] = s;
+}
+
+// ------------------------------------------------------------------ patch im2col
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_kernel(int batch, int C, int H, int W, int P, const T* __restrict__ img,
+                                                     T* __restrict__ out) {
+  const int ph = H / P, pw = W / P;
+  const int64_t cols = (int64_t)C * P * P;
+  const int64_t total = (int64_t)batch * ph * pw * cols;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t prow = o / cols;
+    const int col = (int)(o % cols);
+    const int kx = col % P, ky = (col / P) % P, c = col / (P * P);
+    const int j = (int)(prow % pw), i = (int)((prow / pw) % ph);
+    const int b = (int)(prow / ((int64_t)ph * pw));
+    out[o] = img[(((int64_t)b * C + c) * H + i * P + ky) * W + j * P + kx];
+  }
+}
+
+}  // namespace ops
+}  // namespace mc
+
+using namespace mc;
+using namespace mc::ops;
+
+#define MC_DISPATCH_T(dtype, ...)                                   \
+  do {                                                              \
+    if ((dtype) == MC_DTYPE_F32) { using T = float; __VA_ARGS__; }  \
+    else if ((dtype) == MC_DTYPE_BF16) { using T = bf16_t; __VA_ARGS__; } \
+    else { using T = f16_t; __VA_ARGS__; }                          \
+  } while (0)
+
+static int check_launch(const char* who) {
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "%s: launch failed: %s", who, hipGetErrorString(e));
+  return MC_OK;
+}
+
+extern "C" int mc_add_rmsnorm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, const float* res_in,
+                                  const float* w, float eps, void* y, float* res_out, float* rstd, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_add_rmsnorm_fwd: bad dtype");
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0 && cols / V <= 64 * kMaxVec, MC_ERR_SHAPE,
+           "mc_add_rmsnorm_fwd: cols=%d must be a multiple of %d and <= %d", cols, V, 64 * kMaxVec * V);
+  if (rows == 0) return MC_OK;
+  MC_CHECK(x && w && y && rstd && aligned16(x) && aligned16(y), MC_ERR_INVALID,
+           "mc_add_rmsnorm_fwd: x, w, y, rstd required (x, y 16-B aligned)");
+  const int grid = std::min((rows + 3) / 4, 4096);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_rmsnorm_fwd_kernel<T>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                          rows, cols, (const T*)x, res_in, w, eps, (T*)y, res_out, rstd));
+  return check_launch("mc_add_rmsnorm_fwd");
+}
+
+extern "C" size_t mc_add_rmsnorm_bwd_workspace_bytes(int32_t rows, int32_t cols) {
+  (void)rows;
+  return (size_t)kNormGrid * 4 * cols * sizeof(float);
+}
+
+extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const float* dres,
+                                  const float* h, const float* w, const float* rstd, void* dx, float* dres_in,
+                                  float* dw, void* workspace, size_t workspace_bytes, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_add_rmsnorm_bwd: bad dtype");
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0 && cols / V <= 64 * kMaxVec, MC_ERR_SHAPE,
+           "mc_add_rmsnorm_bwd: bad cols=%d", cols);
+  MC_CHECK(dy && h && w && rstd && dw, MC_ERR_INVALID, "mc_add_rmsnorm_bwd: dy, h, w, rstd, dw required");
+  MC_CHECK(workspace && workspace_bytes >= mc_add_rmsnorm_bwd_workspace_bytes(rows, cols), MC_ERR_WORKSPACE,
+           "mc_add_rmsnorm_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(workspace);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_rmsnorm_bwd_kernel<T>), dim3(kNormGrid), dim3(256), 0, s, rows, cols,
+                                          (const T*)dy, dres, h, w, rstd, (T*)dx, dres_in, part));
+  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, kNormGrid * 4, cols, dw);
+  return check_launch("mc_add_rmsnorm_bwd");
+}
+
+extern "C" int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype,
+                                    const void* x, int64_t x_bs, int64_t x_ds, const float* w, const float* bias,
+                                    int32_t silu, void* y, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_causal_conv1d_fwd: bad dtype");
+  MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0 && K >= 1 && K <= kMaxK, MC_ERR_SHAPE,
+           "mc_causal_conv1d_fwd: bad shape (K must be in [1, %d])", kMaxK);
+  if (batch == 0 || seqlen == 0) return MC_OK;
+  MC_CHECK(x && w && y, MC_ERR_INVALID, "mc_causal_conv1d_fwd: x, w, y required");
+  const int64_t rows = (int64_t)batch * dim;
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((conv1d_fwd_kernel<T>), dim3((rows + 255) / 256), dim3(256), 0,
+                                          (hipStream_t)stream, batch, dim, seqlen, K, (const T*)x, x_bs, x_ds, w, bias,
+                                          silu, (T*)y));
+  return check_launch("mc_causal_conv1d_fwd");
+}
+
+extern "C" size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t K) {
+  (void)K;
+  return (size_t)batch * dim * (kMaxK + 1) * sizeof(float);
+}
+
+extern "C" int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype,
+                                    const void* x, int64_t x_bs, int64_t x_ds, const float* w, const float* bias,
+                                    int32_t silu, const void* dy, void* dx, float* dw, float* dbias, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_causal_conv1d_bwd: bad dtype");
+  MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0 && K >= 1 && K <= kMaxK, MC_ERR_SHAPE, "mc_causal_conv1d_bwd: bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  if (batch == 0 || seqlen == 0) {
+    if (dw) (void)hipMemsetAsync(dw, 0, (size_t)dim * K * 4, s);
+    if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)dim * 4, s);
+    return MC_OK;
+  }
+  MC_CHECK(x && w && dy && dx && dw, MC_ERR_INVALID, "mc_causal_conv1d_bwd: x, w, dy, dx, dw required");
+  MC_CHECK(workspace && workspace_bytes >= mc_causal_conv1d_bwd_workspace_bytes(batch, dim, K), MC_ERR_WORKSPACE,
+           "mc_causal_conv1d_bwd: workspace too small");
+  float* part = reinterpret_cast<float*>(workspace);
+  const int64_t rows = (int64_t)batch * dim;
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((conv1d_bwd_kernel<T>), dim3((rows + 255) / 256), dim3(256), 0, s, batch,
+                                          dim, seqlen, K, (const T*)x, x_bs, x_ds, w, bias, silu, (const T*)dy,
+                                          (T*)dx, part));
+  const int n = dim * (K + 1);
+  hipLaunchKernelGGL(conv1d_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, batch, dim, K, dw, dbias);
+  return check_launch("mc_causal_conv1d_bwd");
+}
+
+extern "C" int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, int32_t P, int32_t dtype,
+                               const void* img, void* patches, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_patch_im2col: bad dtype");
+  MC_CHECK(batch >= 0 && C > 0 && P > 0 && H % P == 0 && W % P == 0, MC_ERR_SHAPE,
+           "mc_patch_im2col: H and W must be multiples of P");
+  if (batch == 0) return MC_OK;
+  MC_CHECK(img && patches, MC_ERR_INVALID, "mc_patch_im2col: null pointer");
+  const int64_t total = (int64_t)batch * C * H * W;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((im2col_kernel<T>), dim3(grid), dim3(256), 0, (hipStream_t)stream, batch,
+                                          C, H, W, P, (const T*)img, (T*)patches));
+  return check_launch("mc_patch_im2col");
+}

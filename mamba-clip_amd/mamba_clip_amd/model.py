@@ -1,0 +1,609 @@
+"""Model-stage-1 / model-stage-2 module API on MI355X.
+
+Mirrors /root/reference/src/mamba_clip/model.py's public surface:
+  ClipModel (model.py:998-1112)      forward(image, text) -> {"image_features", "text_features",
+                                     "logit_scale" (=exp), ["logit_bias"]}; encode_image/encode_text;
+                                     get_logits; lock_text_tower; set_grad_checkpointing
+  ClipClassifier (model.py:1115-1205) frozen stage-1 CLIP + MLP head; classify
+  SS2D / SS_Conv_SSM / VSSLayer / VSSM (model.py:297-995): the MedMamba
+                                     cross-scan vision backbone ("medmamba")
+  init_model (model.py:1257-1289)    factory returning (model, preprocess_train, preprocess_val, tokenizer)
+
+Towers the reference obtains from open_clip / HF hub (not available offline,
+SURVEY.md 8c) are defined here and random-initialised:
+  VisionTransformer  ViT-B/16 (timm vit_base_patch16_224 shape: 12 pre-LN
+                     blocks, 768 wide, cls pooling, proj -> embed_dim)
+  MambaTextEncoder   Mamba LM text tower (Mamba-130M: 24 x d_model 768,
+                     d_inner 1536, d_state 16, RMSNorm, fp32 residual stream)
+  BertTextEncoder    PubMedBERT-base shape (12 x 768, ctx 256) for BiomedCLIP
+Hot ops run on the HIP library: selective scan, causal conv1d, fused
+add+RMSNorm, patch im2col, contrastive loss; dense projections are plain
+library GEMMs (hipBLASLt through torch), attention is torch SDPA.
+"""
+import math
+from functools import partial
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .ops import add_rmsnorm, causal_conv1d, patch_im2col
+from .selective_scan_interface import selective_scan_fn
+
+
+# ============================================================================ Mamba text tower
+def _dt_bias_init(d_inner, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
+    """softplus^-1 of dt ~ logU[dt_min, dt_max] (model.py:459-468 semantics)."""
+    dt = torch.exp(torch.rand(d_inner) * (math.log(dt_max) - math.log(dt_min)) + math.log(dt_min))
+    dt = dt.clamp(min=dt_init_floor)
+    return dt + torch.log(-torch.expm1(-dt))
+
+
+class MambaMixer(nn.Module):
+    """One Mamba mixer: in_proj -> causal conv1d+SiLU -> x_proj/dt_proj -> selective scan (z-gated) -> out_proj.
+
+    Activations stay (batch, channels, seqlen) between the GEMMs so the conv
+    and the scan read unit-stride rows (no transposes on the hot path).
+    """
+
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto"):
+        super().__init__()
+        self.d_model, self.d_state, self.d_conv = d_model, d_state, d_conv
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        self.in_proj = nn.Linear(d_model, 2 * self.d_inner, bias=False)
+        self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, d_conv, groups=self.d_inner, padding=d_conv - 1)
+        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + 2 * d_state, bias=False)
+        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True)
+        std = self.dt_rank ** -0.5
+        nn.init.uniform_(self.dt_proj.weight, -std, std)
+        with torch.no_grad():
+            self.dt_proj.bias.copy_(_dt_bias_init(self.d_inner))
+        A = torch.arange(1, d_state + 1, dtype=torch.float32).repeat(self.d_inner, 1)
+        self.A_log = nn.Parameter(torch.log(A))
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(self.d_inner))
+        self.D._no_weight_decay = True
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=False)
+
+    def forward(self, hidden):  # (B, L, d_model)
+        Bsz, L, _ = hidden.shape
+        dt_in = hidden.dtype
+        w_in = self.in_proj.weight.to(dt_in)
+        xz = torch.matmul(w_in, hidden.transpose(1, 2))                      # (B, 2*d_inner, L)
+        x, z = xz[:, : self.d_inner], xz[:, self.d_inner:]
+        x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True)   # (B, d_inner, L)
+        x_dbl = torch.matmul(self.x_proj.weight.to(dt_in), x)                 # (B, R + 2N, L)
+        dt_raw = x_dbl[:, : self.dt_rank]
+        Bm = x_dbl[:, self.dt_rank: self.dt_rank + self.d_state]
+        Cm = x_dbl[:, self.dt_rank + self.d_state:]
+        delta = torch.matmul(self.dt_proj.weight.to(dt_in), dt_raw)          # (B, d_inner, L)
+        A = -torch.exp(self.A_log.float())
+        y = selective_scan_fn(x, delta, A, Bm, Cm, self.D.float(), z=z,
+                              delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
+        return torch.matmul(y.transpose(1, 2), self.out_proj.weight.to(dt_in).t())   # (B, L, d_model)
+
+
+class MambaLayer(nn.Module):
+    """Pre-norm block: (hidden, residual) -> add+RMSNorm -> mixer (mamba_ssm Block semantics)."""
+
+    def __init__(self, d_model, d_state=16, eps=1e-5):
+        super().__init__()
+        self.mixer = MambaMixer(d_model, d_state=d_state)
+        self.norm_weight = nn.Parameter(torch.ones(d_model))
+        self.eps = eps
+
+    def forward(self, hidden, residual):
+        normed, residual = add_rmsnorm(hidden, residual, self.norm_weight, self.eps)
+        return self.mixer(normed), residual
+
+
+class MambaTextEncoder(nn.Module):
+    """Mamba LM text tower for CLIP: tokens (B, T) int64 -> (B, output_dim).
+
+    Pools the hidden state at the end-of-text position (the last position, as
+    the synthetic tokens put EOT there: SURVEY 8d).  The sequence is padded to
+    a multiple of 8 positions after the real tokens (causal: padding never
+    reaches earlier positions) so every activation row is 16-B aligned.
+    """
+
+    def __init__(self, vocab_size=50280, context_length=77, d_model=768, n_layer=24, d_state=16,
+                 output_dim=512):
+        super().__init__()
+        self.vocab_size, self.context_length, self.d_model = vocab_size, context_length, d_model
+        self.output_dim = output_dim
+        self.embedding = nn.Embedding(vocab_size, d_model)
+        nn.init.normal_(self.embedding.weight, std=0.02)
+        self.layers = nn.ModuleList([MambaLayer(d_model, d_state) for _ in range(n_layer)])
+        self.norm_f = nn.Parameter(torch.ones(d_model))
+        self.proj = nn.Linear(d_model, output_dim, bias=False)
+        nn.init.normal_(self.proj.weight, std=d_model ** -0.5)
+        self.transformer = self.layers  # lock_text_tower walks .transformer (model.py:1072-1097)
+
+    def forward(self, tokens):
+        Bsz, T = tokens.shape
+        Lp = (T + 7) // 8 * 8
+        if Lp != T:
+            tokens = F.pad(tokens, (0, Lp - T))
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+        hidden = self.embedding(tokens).to(dt)
+        residual = None
+        for layer in self.layers:
+            hidden, residual = layer(hidden, residual)
+        normed, _ = add_rmsnorm(hidden, residual, self.norm_f)
+        pooled = normed[:, T - 1]                                   # EOT position
+        return self.proj(pooled)
+
+    def set_grad_checkpointing(self, enable=True):
+        self.grad_checkpointing = enable
+
+
+# ============================================================================ ViT-B/16 visual tower
+class PatchEmbed(nn.Module):
+    """Conv2d(k = s = patch) as im2col (HIP) + one GEMM."""
+
+    def __init__(self, img_size=224, patch=16, in_chans=3, dim=768, bias=True):
+        super().__init__()
+        self.patch, self.grid = patch, img_size // patch
+        self.proj = nn.Conv2d(in_chans, dim, patch, patch, bias=bias)
+
+    def forward(self, x):  # (B, C, H, W) -> (B, H/P * W/P, dim)
+        Bsz = x.shape[0]
+        dt = x.dtype if not torch.is_autocast_enabled("cuda") else torch.get_autocast_dtype("cuda")
+        cols = patch_im2col(x.to(dt), self.patch)
+        w = self.proj.weight.reshape(self.proj.weight.shape[0], -1).to(dt)
+        out = F.linear(cols, w, self.proj.bias.to(dt) if self.proj.bias is not None else None)
+        return out.reshape(Bsz, -1, w.shape[0])
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        Bsz, N, C = x.shape
+        qkv = self.qkv(x).reshape(Bsz, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+        return self.proj(o.transpose(1, 2).reshape(Bsz, N, C))
+
+
+class ViTBlock(nn.Module):
+    def __init__(self, dim, heads, mlp_ratio=4.0):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.fc1 = nn.Linear(dim, int(dim * mlp_ratio))
+        self.fc2 = nn.Linear(int(dim * mlp_ratio), dim)
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        return x + self.fc2(F.gelu(self.fc1(self.norm2(x))))
+
+
+class VisionTransformer(nn.Module):
+    """ViT-B/16 image tower: (B, 3, 224, 224) -> (B, output_dim)."""
+
+    def __init__(self, img_size=224, patch=16, width=768, layers=12, heads=12, output_dim=512):
+        super().__init__()
+        self.output_dim = output_dim
+        self.patch_embed = PatchEmbed(img_size, patch, 3, width)
+        n = (img_size // patch) ** 2
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, width))
+        self.pos_embed = nn.Parameter(torch.randn(1, n + 1, width) * 0.02)
+        self.blocks = nn.ModuleList([ViTBlock(width, heads) for _ in range(layers)])
+        self.norm = nn.LayerNorm(width, eps=1e-6)
+        self.head = nn.Linear(width, output_dim, bias=False)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = self.patch_embed(x)
+        cls = self.cls_token.to(x.dtype).expand(x.shape[0], -1, -1)
+        x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
+        for blk in self.blocks:
+            x = blk(x)
+        return self.head(self.norm(x)[:, 0])
+
+    def lock(self, unlocked_groups=0, freeze_bn_stats=False):
+        for p in self.parameters():
+            p.requires_grad = False
+
+    def set_grad_checkpointing(self, enable=True):
+        self.grad_checkpointing = enable
+
+
+# ============================================================================ BERT text tower (BiomedCLIP shape)
+class BertTextEncoder(nn.Module):
+    """PubMedBERT-base-shaped encoder (12 x 768, ctx 256), CLS pooling + MLP projection."""
+
+    def __init__(self, vocab_size=30522, context_length=256, width=768, layers=12, heads=12, output_dim=512):
+        super().__init__()
+        self.vocab_size, self.context_length, self.output_dim = vocab_size, context_length, output_dim
+        self.tok = nn.Embedding(vocab_size, width)
+        self.pos = nn.Parameter(torch.randn(1, context_length, width) * 0.02)
+        self.ln = nn.LayerNorm(width, eps=1e-12)
+        self.blocks = nn.ModuleList([ViTBlock(width, heads) for _ in range(layers)])
+        self.proj = nn.Sequential(nn.Linear(width, (width + output_dim) // 2, bias=False), nn.GELU(),
+                                  nn.Linear((width + output_dim) // 2, output_dim, bias=False))
+        self.transformer = self.blocks
+
+    def forward(self, tokens):
+        x = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]])
+        for blk in self.blocks:
+            x = blk(x)
+        return self.proj(x[:, 0])
+
+
+# ============================================================================ CLIP wrapper (model.py:998-1112)
+class ClipModel(nn.Module):
+    output_dict = True
+
+    def __init__(self, visual, text, init_logit_scale=math.log(1 / 0.07), init_logit_bias=None):
+        super().__init__()
+        self.output_dict = True
+        self.visual = visual
+        self.text = text
+        self.context_length = getattr(text, "context_length", None)
+        self.vocab_size = getattr(text, "vocab_size", None)
+        self.logit_scale = nn.Parameter(torch.ones([]) * init_logit_scale)
+        self.logit_bias = nn.Parameter(torch.ones([]) * init_logit_bias) if init_logit_bias is not None else None
+
+    def encode_image(self, image, normalize: bool = False):
+        f = self.visual(image)
+        return F.normalize(f, dim=-1) if normalize else f
+
+    def encode_text(self, text, normalize: bool = False):
+        f = self.text(text)
+        return F.normalize(f, dim=-1) if normalize else f
+
+    def forward(self, image, text, secondary_text=None):
+        image_features = self.encode_image(image, normalize=True) if image is not None else None
+        text_features = self.encode_text(text, normalize=True) if text is not None else None
+        secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
+        if self.output_dict:
+            out = {"image_features": image_features, "text_features": text_features,
+                   "logit_scale": self.logit_scale.exp()}
+            if secondary is not None:
+                out["secondary_text_features"] = secondary
+            if self.logit_bias is not None:
+                out["logit_bias"] = self.logit_bias
+            return out
+        out = (image_features, text_features, self.logit_scale.exp())
+        if secondary is not None:
+            out += (secondary,)
+        if self.logit_bias is not None:
+            out += (self.logit_bias,)
+        return out
+
+    def lock_image_tower(self, unlocked_groups=0, freeze_bn_stats=False):
+        self.visual.lock(unlocked_groups=unlocked_groups, freeze_bn_stats=freeze_bn_stats)
+
+    def lock_text_tower(self, unlocked_layers: int = 0, freeze_layer_norm: bool = True):
+        layers = list(getattr(self.text, "transformer", []))
+        frozen = layers if not unlocked_layers else layers[:-unlocked_layers]
+        for m in frozen:
+            for n, p in m.named_parameters():
+                p.requires_grad = (not freeze_layer_norm) and ("norm" in n.lower())
+
+    def set_grad_checkpointing(self, enable=True):
+        for t in (self.visual, self.text):
+            if hasattr(t, "set_grad_checkpointing"):
+                t.set_grad_checkpointing(enable)
+
+    def get_logits(self, image, text):
+        from .ops import gemm_nt
+        i = self.encode_image(image, normalize=True)
+        t = self.encode_text(text, normalize=True)
+        dt = i.dtype if i.dtype == torch.bfloat16 else torch.float32
+        image_logits = gemm_nt(i.to(dt), t.to(dt), alpha_dev=self.logit_scale.exp().float().reshape(()))
+        if self.logit_bias is not None:
+            image_logits = image_logits + self.logit_bias
+        return image_logits, image_logits.T
+
+
+# ============================================================================ stage-2 head (model.py:1115-1205)
+def unwrap_model(m):
+    return m.module if hasattr(m, "module") else m
+
+
+class ClipClassifier(nn.Module):
+    def __init__(self, clip_model, feature_dim=None, num_classes: int = 2, use_visual_only=False,
+                 use_text_only=False, use_inner_prod=False):
+        super().__init__()
+        self.clip_model = unwrap_model(clip_model)
+        self.num_classes = num_classes
+        for p in self.clip_model.parameters():
+            p.requires_grad = False
+        if feature_dim is None:
+            i_dim = getattr(self.clip_model.visual, "output_dim", None)
+            t_dim = getattr(self.clip_model.text, "output_dim", None)
+            if i_dim is None or t_dim is None:
+                raise ValueError("Could not find image and text feature dimensions in the model")
+            feature_dim = i_dim + t_dim
+        self.use_visual_only, self.use_text_only, self.use_inner_prod = use_visual_only, use_text_only, use_inner_prod
+        out_dim = feature_dim if (use_visual_only or use_text_only or use_inner_prod) else feature_dim // 2
+        self.fc = nn.Sequential(nn.Linear(feature_dim, out_dim), nn.ReLU(), nn.Linear(out_dim, num_classes))
+
+    def forward(self, image, text):
+        with torch.no_grad():
+            out = self.clip_model(image, text)
+        i, t = out["image_features"], out["text_features"]
+        if self.use_visual_only:
+            return self.fc(i.float())
+        if self.use_text_only:
+            return self.fc(t.float())
+        if self.use_inner_prod:
+            return self.fc((i * t).float())
+        return self.fc(torch.cat((i, t), dim=1).float())
+
+    def get_logits(self, image_features, text_features):
+        # the reference's clup_model typo (Appendix A.6) is not reproduced
+        logits = image_features * text_features
+        if self.clip_model.logit_bias is not None:
+            logits = logits + self.clip_model.logit_bias
+        return logits
+
+    def classify(self, image, text):
+        probabilities = F.softmax(self.forward(image, text), dim=1)
+        return torch.argmax(probabilities, dim=1), probabilities
+
+
+# ============================================================================ MedMamba / VSSM (model.py:174-995)
+class PatchEmbed2D(nn.Module):
+    """Conv2d k = s = patch (model.py:174-201) as im2col + GEMM, channels-last output."""
+
+    def __init__(self, patch_size=4, in_chans=3, embed_dim=96, norm_layer=None, **kwargs):
+        super().__init__()
+        self.patch = patch_size if isinstance(patch_size, int) else patch_size[0]
+        self.proj = nn.Conv2d(in_chans, embed_dim, self.patch, self.patch)
+        self.norm = norm_layer(embed_dim) if norm_layer is not None else None
+
+    def forward(self, x):
+        Bsz, _, H, W = x.shape
+        cols = patch_im2col(x, self.patch)
+        w = self.proj.weight.reshape(self.proj.weight.shape[0], -1).to(cols.dtype)
+        y = F.linear(cols, w, self.proj.bias.to(cols.dtype)).reshape(Bsz, H // self.patch, W // self.patch, -1)
+        return self.norm(y) if self.norm is not None else y
+
+
+class PatchMerging2D(nn.Module):
+    """2x2 neighbourhood concat -> LN -> Linear(4C, 2C) (model.py:204-246)."""
+
+    def __init__(self, dim, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.dim = dim
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+        self.norm = norm_layer(4 * dim)
+
+    def forward(self, x):
+        Bsz, H, W, C = x.shape
+        h2, w2 = H // 2, W // 2
+        parts = [x[:, 0::2, 0::2], x[:, 1::2, 0::2], x[:, 0::2, 1::2], x[:, 1::2, 1::2]]
+        x = torch.cat([p[:, :h2, :w2] for p in parts], -1)
+        return self.reduction(self.norm(x))
+
+
+class SS2D(nn.Module):
+    """2-D selective scan over four directions (model.py:297-647), scan on the HIP kernel.
+
+    Parameter names/shapes match the reference so its state dicts load as-is.
+    """
+
+    def __init__(self, d_model, d_state=16, d_conv=3, expand=2, dt_rank="auto", dt_min=0.001, dt_max=0.1,
+                 dt_init="random", dt_scale=1.0, dt_init_floor=1e-4, dropout=0.0, conv_bias=True, bias=False,
+                 **kwargs):
+        super().__init__()
+        self.d_model, self.d_state, self.d_conv, self.expand = d_model, d_state, d_conv, expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        K, di, R, N = 4, self.d_inner, self.dt_rank, d_state
+        self.in_proj = nn.Linear(d_model, 2 * di, bias=bias)
+        self.conv2d = nn.Conv2d(di, di, d_conv, groups=di, bias=conv_bias, padding=(d_conv - 1) // 2)
+        self.act = nn.SiLU()
+        xw = torch.empty(K, R + 2 * N, di)
+        for k in range(K):
+            nn.init.kaiming_uniform_(xw[k], a=math.sqrt(5))
+        self.x_proj_weight = nn.Parameter(xw)
+        std = R ** -0.5 * dt_scale
+        dtw = torch.empty(K, di, R)
+        if dt_init == "constant":
+            nn.init.constant_(dtw, std)
+        elif dt_init == "random":
+            nn.init.uniform_(dtw, -std, std)
+        else:
+            raise NotImplementedError
+        self.dt_projs_weight = nn.Parameter(dtw)
+        self.dt_projs_bias = nn.Parameter(torch.stack([_dt_bias_init(di, dt_min, dt_max, dt_init_floor)
+                                                       for _ in range(K)]))
+        A = torch.arange(1, N + 1, dtype=torch.float32).repeat(K * di, 1)
+        self.A_logs = nn.Parameter(torch.log(A))
+        self.A_logs._no_weight_decay = True
+        self.Ds = nn.Parameter(torch.ones(K * di))
+        self.Ds._no_weight_decay = True
+        self.out_norm = nn.LayerNorm(di)
+        self.out_proj = nn.Linear(di, d_model, bias=bias)
+        self.dropout = nn.Dropout(dropout) if dropout > 0.0 else None
+
+    def forward_core(self, x):  # (B, d, H, W) -> four (B, d, L) maps, fp32
+        Bsz, d, H, W = x.shape
+        L, K = H * W, 4
+        x_hw = x.reshape(Bsz, d, L)
+        x_wh = x.transpose(2, 3).reshape(Bsz, d, L)
+        xs = torch.stack([x_hw, x_wh, x_hw.flip(-1), x_wh.flip(-1)], dim=1)          # (B, K, d, L)
+        x_dbl = torch.einsum("bkdl,kcd->bkcl", xs, self.x_proj_weight.to(xs.dtype))
+        dts, Bs, Cs = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=2)
+        dts = torch.einsum("bkrl,kdr->bkdl", dts, self.dt_projs_weight.to(xs.dtype))
+        out = selective_scan_fn(xs.float().reshape(Bsz, K * d, L), dts.float().reshape(Bsz, K * d, L),
+                                -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
+                                z=None, delta_bias=self.dt_projs_bias.float().reshape(-1), delta_softplus=True)
+        out = out.reshape(Bsz, K, d, L)
+        y_inv = out[:, 2:4].flip(-1)
+        y_wh = out[:, 1].reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, L)
+        y_invwh = y_inv[:, 1].reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, L)
+        return out[:, 0], y_inv[:, 0], y_wh, y_invwh
+
+    def forward(self, x, **kwargs):  # (B, H, W, C)
+        Bsz, H, W, _ = x.shape
+        x, z = self.in_proj(x).chunk(2, dim=-1)
+        x = self.act(self.conv2d(x.permute(0, 3, 1, 2).contiguous()))
+        y1, y2, y3, y4 = self.forward_core(x)
+        y = (y1 + y2 + y3 + y4).transpose(1, 2).reshape(Bsz, H, W, -1)
+        y = self.out_norm(y) * F.silu(z)
+        out = self.out_proj(y)
+        return self.dropout(out) if self.dropout is not None else out
+
+
+def channel_shuffle(x, groups):
+    Bsz, H, W, C = x.shape
+    return x.view(Bsz, H, W, groups, C // groups).transpose(3, 4).reshape(Bsz, H, W, C)
+
+
+class SS_Conv_SSM(nn.Module):
+    """Half the channels through a conv stack, half through SS2D; shuffle; residual (model.py:666-723)."""
+
+    def __init__(self, hidden_dim=0, drop_path=0.0, norm_layer=partial(nn.LayerNorm, eps=1e-6), attn_drop_rate=0.0,
+                 d_state=16, **kwargs):
+        super().__init__()
+        h = hidden_dim // 2
+        self.ln_1 = norm_layer(h)
+        self.self_attention = SS2D(d_model=h, dropout=attn_drop_rate, d_state=d_state, **kwargs)
+        self.drop_path = nn.Identity() if drop_path == 0 else _DropPath(drop_path)
+        self.conv33conv33conv11 = nn.Sequential(
+            nn.BatchNorm2d(h), nn.Conv2d(h, h, 3, 1, 1), nn.BatchNorm2d(h), nn.ReLU(),
+            nn.Conv2d(h, h, 3, 1, 1), nn.BatchNorm2d(h), nn.ReLU(), nn.Conv2d(h, h, 1, 1), nn.ReLU())
+
+    def forward(self, inp):
+        left, right = inp.chunk(2, dim=-1)
+        x = self.drop_path(self.self_attention(self.ln_1(right)))
+        left = self.conv33conv33conv11(left.permute(0, 3, 1, 2).contiguous()).permute(0, 2, 3, 1).contiguous()
+        return channel_shuffle(torch.cat((left, x), dim=-1), groups=2) + inp
+
+
+class _DropPath(nn.Module):
+    def __init__(self, p):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        if not self.training or self.p == 0.0:
+            return x
+        keep = x.new_empty((x.shape[0],) + (1,) * (x.dim() - 1)).bernoulli_(1 - self.p)
+        return x * keep / (1 - self.p)
+
+
+class VSSLayer(nn.Module):
+    def __init__(self, dim, depth, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm, downsample=None,
+                 use_checkpoint=False, d_state=16, **kwargs):
+        super().__init__()
+        self.dim, self.use_checkpoint = dim, use_checkpoint
+        self.blocks = nn.ModuleList([
+            SS_Conv_SSM(hidden_dim=dim, drop_path=drop_path[i] if isinstance(drop_path, list) else drop_path,
+                        norm_layer=norm_layer, attn_drop_rate=attn_drop, d_state=d_state)
+            for i in range(depth)])
+        self.downsample = downsample(dim=dim, norm_layer=norm_layer) if downsample is not None else None
+
+    def forward(self, x):
+        for blk in self.blocks:
+            x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False) if self.use_checkpoint else blk(x)
+        return self.downsample(x) if self.downsample is not None else x
+
+
+class VSSM(nn.Module):
+    """MedMamba backbone + head (model.py:868-995); "medmamba" = depths [2,2,8,2], dims [64,128,256,512]."""
+
+    def __init__(self, patch_size=4, in_chans=3, num_classes=1000, depths=(2, 2, 4, 2), dims=(96, 192, 384, 768),
+                 d_state=16, drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=nn.LayerNorm,
+                 patch_norm=True, use_checkpoint=False, **kwargs):
+        super().__init__()
+        depths, dims = list(depths), list(dims)
+        self.num_classes, self.num_layers = num_classes, len(depths)
+        self.embed_dim, self.num_features, self.dims = dims[0], dims[-1], dims
+        self.patch_embed = PatchEmbed2D(patch_size, in_chans, dims[0], norm_layer if patch_norm else None)
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        dpr = [v.item() for v in torch.linspace(0, drop_path_rate, sum(depths))]
+        self.layers = nn.ModuleList([
+            VSSLayer(dims[i], depths[i], d_state=math.ceil(dims[0] / 6) if d_state is None else d_state,
+                     attn_drop=attn_drop_rate, drop_path=dpr[sum(depths[:i]): sum(depths[: i + 1])],
+                     norm_layer=norm_layer, downsample=PatchMerging2D if i < self.num_layers - 1 else None,
+                     use_checkpoint=use_checkpoint)
+            for i in range(self.num_layers)])
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.head = nn.Linear(self.num_features, num_classes) if num_classes > 0 else nn.Identity()
+        self.output_dim = num_classes if num_classes > 0 else self.num_features
+        self.apply(self._init_weights)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    @staticmethod
+    def _init_weights(m):
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def forward_backbone(self, x):
+        x = self.pos_drop(self.patch_embed(x))
+        for layer in self.layers:
+            x = layer(x)
+        return x
+
+    def forward(self, x):
+        x = self.forward_backbone(x).permute(0, 3, 1, 2)
+        return self.head(torch.flatten(self.avgpool(x), 1))
+
+
+# ============================================================================ factory (model.py:1257-1289)
+MODEL_CONFIGS = {
+    # C1: tiny plumbing config (BASELINE configs[0])
+    "tiny-mamba-clip": dict(vision=dict(img_size=32, patch=8, width=64, layers=2, heads=4, output_dim=32),
+                            text=dict(vocab_size=1000, context_length=16, d_model=128, n_layer=2, output_dim=32)),
+    # C2: ViT-B/16 + Mamba-130M text (BASELINE configs[1])
+    "vit_b16-mamba130m": dict(vision=dict(), text=dict(vocab_size=50280, context_length=77, d_model=768,
+                                                        n_layer=24, output_dim=512)),
+    # C4 text tower (BASELINE configs[3])
+    "mamba790m-text": dict(vision=dict(), text=dict(vocab_size=50280, context_length=4096, d_model=1536,
+                                                     n_layer=48, output_dim=512)),
+    # C3: BiomedCLIP-shaped (ViT-B/16 + PubMedBERT-256), random init (BASELINE configs[2])
+    "biomedclip-vit_b16-pubmedbert256": dict(vision=dict(), bert=dict()),
+}
+
+
+def build_clip(name):
+    cfg = MODEL_CONFIGS[name]
+    visual = VisionTransformer(**cfg["vision"])
+    text = BertTextEncoder(**cfg["bert"]) if "bert" in cfg else MambaTextEncoder(**cfg["text"])
+    return ClipModel(visual, text)
+
+
+def init_model(model, tokenizer=None, aug_cfg=None, is_clip=False, use_tokenizer=False):
+    """Returns (model, preprocess_train, preprocess_val, tokenizer) like model.py:1257-1289.
+
+    "medmamba" -> VSSM(depths=[2,2,8,2], dims=[64,128,256,512], num_classes=2);
+    a MODEL_CONFIGS name -> a random-init ClipModel (no hub access offline);
+    a callable -> model().  Preprocessing is identity on synthetic tensors.
+    """
+    if model == "medmamba":
+        model = VSSM(depths=[2, 2, 8, 2], dims=[64, 128, 256, 512], num_classes=2)
+    elif isinstance(model, str):
+        if model not in MODEL_CONFIGS:
+            raise ValueError(f"unknown model {model!r}: offline build knows {sorted(MODEL_CONFIGS)}")
+        model = build_clip(model)
+    elif callable(model):
+        model = model()
+    if is_clip and not isinstance(model, ClipModel):
+        model = ClipModel(model.visual, model.text)
+    if use_tokenizer and tokenizer is not None and callable(tokenizer):
+        tokenizer = tokenizer()
+    identity = (lambda x: x)
+    return model, identity, identity, tokenizer

@@ -112,3 +112,105 @@ class ScaledLogitsCE(torch.autograd.Function):
 
 def scaled_logits_ce(X, Y, scale, row_off=0, coef_r=1.0, col_off=0, coef_c=0.0):
     return ScaledLogitsCE.apply(X, Y, scale, row_off, coef_r, col_off, coef_c)
+
+
+# ---------------------------------------------------------------------------- encoder ops (include/mc_ops.h)
+class AddRMSNormFn(torch.autograd.Function):
+    """(y, h) = (rmsnorm(x + res) * w, x + res); h is the fp32 residual stream."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, eps):
+        lib = _lib.load()
+        x = x.contiguous()
+        rows = x.numel() // x.shape[-1]
+        cols = x.shape[-1]
+        y = torch.empty_like(x)
+        h = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        w = weight.float().contiguous()
+        r = res.float().contiguous() if res is not None else None
+        _lib.check(lib.mc_add_rmsnorm_fwd(rows, cols, _lib.dtype_code(x.dtype), x.data_ptr(), _lib.ptr(r),
+                                          w.data_ptr(), float(eps), y.data_ptr(), h.data_ptr(), rstd.data_ptr(),
+                                          _lib.stream_handle(x.device)), "mc_add_rmsnorm_fwd")
+        ctx.save_for_backward(h, w, rstd)
+        ctx.meta = (x.dtype, res is not None, weight.dtype)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh_out):
+        lib = _lib.load()
+        h, w, rstd = ctx.saved_tensors
+        xdt, has_res, wdt = ctx.meta
+        cols = h.shape[-1]
+        rows = h.numel() // cols
+        dy = (dy if dy is not None else torch.zeros(h.shape, device=h.device, dtype=xdt)).to(xdt).contiguous()
+        dres = dh_out.float().contiguous() if dh_out is not None else None
+        dx = torch.empty(h.shape, device=h.device, dtype=xdt)
+        dres_in = torch.empty_like(h) if has_res else None
+        dw = torch.empty(cols, device=h.device, dtype=torch.float32)
+        ws_b = lib.mc_add_rmsnorm_bwd_workspace_bytes(rows, cols)
+        ws = _ws(ws_b, h.device)
+        _lib.check(lib.mc_add_rmsnorm_bwd(rows, cols, _lib.dtype_code(xdt), dy.data_ptr(), _lib.ptr(dres),
+                                          h.data_ptr(), w.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                          _lib.ptr(dres_in), dw.data_ptr(), ws.data_ptr(), ws_b,
+                                          _lib.stream_handle(h.device)), "mc_add_rmsnorm_bwd")
+        return dx, dres_in, dw.to(wdt), None
+
+
+def add_rmsnorm(x, residual, weight, eps=1e-5):
+    return AddRMSNormFn.apply(x, residual, weight, eps)
+
+
+class CausalConv1dFn(torch.autograd.Function):
+    """Depthwise causal conv1d (+SiLU) over (batch, dim, seqlen); output contiguous."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, silu):
+        lib = _lib.load()
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        Bsz, D, L = x.shape
+        K = weight.shape[-1]
+        w = weight.reshape(D, K).float().contiguous()
+        b = bias.float().contiguous() if bias is not None else None
+        y = torch.empty(Bsz, D, L, device=x.device, dtype=x.dtype)
+        _lib.check(lib.mc_causal_conv1d_fwd(Bsz, D, L, K, _lib.dtype_code(x.dtype), x.data_ptr(), x.stride(0),
+                                            x.stride(1), w.data_ptr(), _lib.ptr(b), int(silu), y.data_ptr(),
+                                            _lib.stream_handle(x.device)), "mc_causal_conv1d_fwd")
+        ctx.save_for_backward(x, w, b if b is not None else w)
+        ctx.meta = (silu, bias is not None, weight.shape, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.load()
+        x, w, b = ctx.saved_tensors
+        silu, has_b, wshape, wdt = ctx.meta
+        Bsz, D, L = x.shape
+        K = w.shape[-1]
+        dy = dy.to(x.dtype).contiguous()
+        dx = torch.empty(Bsz, D, L, device=x.device, dtype=x.dtype)
+        dw = torch.empty(D, K, device=x.device, dtype=torch.float32)
+        db = torch.empty(D, device=x.device, dtype=torch.float32) if has_b else None
+        ws_b = lib.mc_causal_conv1d_bwd_workspace_bytes(Bsz, D, K)
+        ws = _ws(ws_b, x.device)
+        _lib.check(lib.mc_causal_conv1d_bwd(Bsz, D, L, K, _lib.dtype_code(x.dtype), x.data_ptr(), x.stride(0),
+                                            x.stride(1), w.data_ptr(), b.data_ptr() if has_b else None, int(silu),
+                                            dy.data_ptr(), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(),
+                                            ws_b, _lib.stream_handle(x.device)), "mc_causal_conv1d_bwd")
+        return dx, dw.reshape(wshape).to(wdt), (db.to(wdt) if db is not None else None), None
+
+
+def causal_conv1d(x, weight, bias=None, silu=True):
+    return CausalConv1dFn.apply(x, weight, bias, silu)
+
+
+def patch_im2col(img, patch):
+    """(B, C, H, W) -> (B * H/P * W/P, C * P * P) patch rows (no autograd: image inputs)."""
+    lib = _lib.load()
+    img = img.contiguous()
+    Bsz, C, H, W = img.shape
+    out = torch.empty(Bsz * (H // patch) * (W // patch), C * patch * patch, device=img.device, dtype=img.dtype)
+    _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(img.dtype), img.data_ptr(), out.data_ptr(),
+                                   _lib.stream_handle(img.device)), "mc_patch_im2col")
+    return out
