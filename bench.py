@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json metric): image-text pairs/sec + selective_scan HBM GB/s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload (value): C2 = ViT-B/16 image tower + Mamba-130M text tower, 224x224
+synthetic images + 77-token synthetic text, batch 256 per GPU, bf16 autocast,
+full step = forward + ClipLoss (HIP contrastive kernels; RCCL feature
+all-gather for N > 1) + backward (DDP RCCL all-reduce) + fused AdamW +
+logit_scale clamp.  Random-init weights, synthetic data resident in HBM.
+value = N * batch * K / max-over-ranks(time of K steps).
+
+roofline: the selective-scan forward at C4 (B=64, D=3072, L=4096, N=16, bf16,
+z-gated, softplus) -- the kernel BASELINE.json's HBM target
+names -- timed with HIP events on the stream it is launched on;
+achieved = 6.4594 GB algorithmic bytes per call / average call time.
+
+cpu_baseline: the fp32 CPU restatement (oracle/cpu_model.py) of the same
+C2 training step on a bounded sample (batch 8), rank 0 at N = 1 only.
+
+For N > 1 run under torch.distributed.run (one process per GPU, RCCL);
+`--gpus N` without a launcher re-launches itself as a child torchrun job.
+"""
+import argparse
+import json
+import math
+import os
+import socket
+import subprocess
+import sys
+import time
+from types import SimpleNamespace
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (MI355X_MICROARCH.md)
+MFMA_BF16_DENSE_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+C2_FLOP_PER_PAIR = 146e9         # fwd+bwd, SURVEY.md 8(d)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="pairs per GPU")
+    ap.add_argument("--model", default="vit_b16-mamba130m")
+    ap.add_argument("--scan-iters", type=int, default=20)
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(args):
+    """--gpus N > 1 without a launcher: run torchrun as a child and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def scan_roofline(iters, warmup=3):
+    """selective_scan_fwd at C4 timed with HIP events on its launch stream."""
+    import torch
+    from mamba_clip_amd.selective_scan_interface import scan_fwd
+    dev = torch.device("cuda", torch.cuda.current_device())
+    Bsz, D, L, N = 64, 3072, 4096, 16
+    g = torch.Generator(device=dev).manual_seed(0)
+    bf = torch.bfloat16
+    u = torch.randn(Bsz, D, L, device=dev, generator=g, dtype=bf)
+    z = torch.randn(Bsz, D, L, device=dev, generator=g, dtype=bf)
+    delta = (torch.randn(Bsz, D, L, device=dev, generator=g) * 0.5).to(bf)
+    dt = torch.exp(torch.rand(D, device=dev, generator=g) * (math.log(0.1) - math.log(1e-3)) + math.log(1e-3))
+    dt = dt.clamp(min=1e-4)
+    bias = dt + torch.log(-torch.expm1(-dt))
+    A = -torch.exp(torch.log(torch.arange(1, N + 1, device=dev, dtype=torch.float32)).repeat(D, 1)
+                   + 0.1 * torch.randn(D, N, device=dev, generator=g))
+    Bm = torch.randn(Bsz, 1, N, L, device=dev, generator=g, dtype=bf)
+    Cm = torch.randn(Bsz, 1, N, L, device=dev, generator=g, dtype=bf)
+    Dv = torch.ones(D, device=dev)
+    call = lambda: scan_fwd(u, delta, A, Bm, Cm, Dv, z, bias, True, False, False)  # noqa: E731
+    for _ in range(warmup):
+        call()
+    stream = torch.cuda.current_stream(dev)      # the lib launches on torch's current stream
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    t0.record(stream)
+    for _ in range(iters):
+        call()
+    t1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = t0.elapsed_time(t1) / iters
+    nbytes = Bsz * D * L * 8 + 2 * Bsz * 1 * N * L * 2 + (D * N + 2 * D) * 4
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    del u, z, delta, Bm, Cm
+    torch.cuda.empty_cache()
+    return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+
+
+def cpu_baseline(args, model_name):
+    import torch
+    from oracle.cpu_model import cpu_train_pairs_per_sec
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    pps, secs = cpu_train_pairs_per_sec(model_name, batch=args.cpu_batch, steps=args.cpu_steps, warmup=1,
+                                        threads=threads)
+    torch.set_num_threads(prev)
+    return {"value": round(pps, 4), "unit": "image-text pairs/sec", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} timed fp32 CPU train steps (+1 warmup) of {model_name} at batch "
+                      f"{args.cpu_batch} via oracle/cpu_model.py ({secs:.1f} s timed)"}
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
+
+    import torch
+    import torch.distributed as dist
+
+    from mamba_clip_amd import _lib
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import build_clip
+    from mamba_clip_amd.train import create_optimizer, train_step, wrap_ddp
+    from mamba_clip_amd.utils import init_device
+
+    _lib.load()                                   # fail loudly if the HIP library is missing
+    targs = SimpleNamespace(precision="amp_bf16", lr=5e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
+                            grad_clip_norm=None, dist_backend="nccl", ddp_static_graph=True, accum_freq=1)
+    device = init_device(targs)
+    rank, world = targs.rank, targs.world_size
+    targs.lr *= world                             # pipeline.py:532
+
+    torch.manual_seed(0)
+    model = build_clip(args.model).to(device)
+    model = wrap_ddp(model, targs, device)
+    optimizer = create_optimizer(model, targs)
+    loss = ClipLoss(rank=rank, world_size=world)
+    inner = model.module if hasattr(model, "module") else model
+    images, texts, targets = synthetic_batch(args.batch, 224, inner.text.context_length, inner.text.vocab_size,
+                                             device=device, seed=1000 + rank)
+    model.train()
+
+    def step():
+        return train_step(model, images, texts, targets, loss, optimizer, None, targs)
+
+    for _ in range(args.warmup):
+        losses = step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    final_loss = float(losses["loss"].item())
+    if not math.isfinite(final_loss):
+        raise RuntimeError(f"non-finite training loss {final_loss}")
+
+    value = world * args.batch * args.steps / elapsed
+    result = {
+        "metric": "image-text pairs/sec (whole node) + selective_scan HBM GB/s",
+        "value": round(value, 2), "unit": "image-text pairs/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) 77-token text, EOT last)",
+        "config": {"workload": "C2: ViT-B/16 image + Mamba-130M text, contrastive train step "
+                               "(fwd+bwd+AdamW), amp_bf16",
+                   "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                   "seq_len": int(inner.text.context_length), "image_size": 224,
+                   "parallelism": f"dp{world}"},
+        "mfma_estimate": {"flop_per_pair": C2_FLOP_PER_PAIR,
+                          "achieved_tflops_per_gpu": round(value / world * C2_FLOP_PER_PAIR / 1e12, 1),
+                          "peak": MFMA_BF16_DENSE_TFLOPS,
+                          "frac": round(value / world * C2_FLOP_PER_PAIR / 1e12 / MFMA_BF16_DENSE_TFLOPS, 4)},
+        "final_loss": round(final_loss, 5),
+    }
+    del images, texts, targets, optimizer
+    torch.cuda.empty_cache()
+    if rank == 0 and not args.no_roofline:
+        result["roofline"] = scan_roofline(args.scan_iters)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, args.model)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+"""Stage-1 CLIP training step on MI355X (reference: src/mamba_clip/train.py:92-372, pipeline.py:266-311).
+
+One optimizer step = scheduler(step) -> zero_grad -> autocast forward of both
+towers -> ClipLoss (HIP contrastive kernels, RCCL feature all-gather) ->
+backward (DDP bucketed RCCL all-reduce overlapped with the tail of backward)
+-> optional grad clip -> AdamW -> logit_scale.clamp_(0, ln 100).
+
+Differences from the reference are deliberate fixes:
+balanced-mixup variables are only touched when balanced mixup is on (A.2),
+and the accumulation path passes the concatenated features to the loss (the
+reference builds `inputs` and then ignores it).
+"""
+import logging
+import math
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .utils.amp_utils import get_autocast, get_input_dtype
+from .utils.dist_utils import is_master
+
+
+class AverageMeter:
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = self.avg = self.sum = 0.0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+def unwrap_model(model):
+    return model.module if hasattr(model, "module") else model
+
+
+def postprocess_clip_output(model_out):
+    return {"image_features": model_out[0], "text_features": model_out[1], "logit_scale": model_out[2]}
+
+
+def backward(total_loss, scaler):
+    if scaler is not None:
+        scaler.scale(total_loss).backward()
+    else:
+        total_loss.backward()
+
+
+def get_model_inputs(args, images, texts, targets=None, balanced_images=None, balanced_texts=None,
+                     balanced_targets=None):
+    """train.py:66-89: optional balanced mixup, then (images,) or (images, texts)."""
+    if getattr(args, "balanced_mixup", None):
+        lam = np.random.beta(a=args.balanced_mixup, b=1)
+        images = (1 - lam) * images + lam * balanced_images
+        if lam > 0.5 and texts is not None and balanced_texts is not None:
+            texts = balanced_texts
+        n_classes = args.num_classes
+        targets = F.one_hot(targets, n_classes)
+        targets = (1 - lam) * targets + lam * F.one_hot(balanced_targets, n_classes)
+    return (images,) if texts is None else (images, texts)
+
+
+# ---------------------------------------------------------------- optimizer / DDP (pipeline.py:266-311)
+def _no_decay(name, p):
+    return p.ndim < 2 or "bn" in name or "ln" in name or "bias" in name or "logit_scale" in name
+
+
+def create_optimizer(model, args):
+    """AdamW with two groups: gains/biases/logit_scale at wd 0, the rest at args.wd.
+
+    On the GPU the fused (single multi-tensor kernel) AdamW is used: same update
+    rule as torch.optim.AdamW's foreach path, one launch per step.
+    """
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    groups = [{"params": [p for n, p in named if _no_decay(n, p)], "weight_decay": 0.0},
+              {"params": [p for n, p in named if not _no_decay(n, p)], "weight_decay": args.wd}]
+    on_gpu = all(p.is_cuda for _, p in named)
+    return torch.optim.AdamW(groups, lr=args.lr, betas=(args.beta1, args.beta2), eps=args.eps,
+                             fused=True if on_gpu else None)
+
+
+def create_scaler(args, device):
+    if args.precision != "amp":
+        return None
+    return torch.amp.GradScaler("cuda" if device.type == "cuda" else "cpu")
+
+
+def wrap_ddp(model, args, device):
+    """One process per GPU; gradients all-reduced over RCCL in 100 MB buckets during backward."""
+    if not getattr(args, "distributed", False):
+        return model
+    kw = dict(static_graph=getattr(args, "ddp_static_graph", False), gradient_as_bucket_view=True,
+              bucket_cap_mb=getattr(args, "ddp_bucket_mb", 100))
+    if device.type == "cuda":
+        kw["device_ids"] = [device]
+    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+
+
+# ---------------------------------------------------------------- one optimizer step
+def _loss_terms(loss, model_out, targets):
+    if isinstance(model_out, dict) and "logits" in model_out:
+        model_out = {"input": model_out["logits"]}
+    elif not isinstance(model_out, dict):
+        model_out = {"input": model_out}
+    losses = loss(**model_out, target=targets)
+    if isinstance(losses, dict):
+        total = sum(losses.values())
+        losses["loss"] = total
+    else:
+        total, losses = losses, {"loss": losses}
+    return total, losses
+
+
+def optimizer_step(model, optimizer, scaler, args):
+    """train.py:292-315: (unscale, clip,) step, then clamp logit_scale to [0, ln 100]."""
+    clip = getattr(args, "grad_clip_norm", None)
+    if scaler is not None:
+        if clip is not None:
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), clip, norm_type=2.0)
+        scaler.step(optimizer)
+        scaler.update()
+    else:
+        if clip is not None:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), clip, norm_type=2.0)
+        optimizer.step()
+    inner = unwrap_model(model)
+    if hasattr(inner, "logit_scale"):
+        with torch.no_grad():
+            inner.logit_scale.clamp_(0, math.log(100))
+
+
+def train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast=None):
+    """One accum_freq == 1 step on device-resident inputs; returns the loss dict (device tensors)."""
+    autocast = autocast or get_autocast(args.precision)
+    optimizer.zero_grad(set_to_none=True)
+    with autocast():
+        model_out = model(*get_model_inputs(args, images, texts, targets))
+        total, losses = _loss_terms(loss, model_out, targets)
+    backward(total, scaler)
+    optimizer_step(model, optimizer, scaler, args)
+    return losses
+
+
+def train_step_accum(model, batches, loss, optimizer, scaler, args, autocast=None):
+    """Gradient-cache accumulation over `batches` (train.py:218-291).
+
+    Features of every micro-batch are computed without grad; then each micro-batch
+    is re-run with grad and its loss uses the other micro-batches' cached
+    features as extra negatives.
+    """
+    autocast = autocast or get_autocast(args.precision)
+    cached = {}
+    with torch.no_grad(), autocast():
+        for images, texts, targets in batches:
+            out = model(*get_model_inputs(args, images, texts, targets))
+            for k, v in out.items():
+                if k not in ("logit_scale", "logit_bias"):
+                    cached.setdefault(k, []).append(v)
+    optimizer.zero_grad(set_to_none=True)
+    losses = None
+    for j, (images, texts, targets) in enumerate(batches):
+        with autocast():
+            out = model(*get_model_inputs(args, images, texts, targets))
+            inputs = {k: out[k] for k in ("logit_scale", "logit_bias") if k in out}
+            for k, vals in cached.items():
+                inputs[k] = torch.cat(vals[:j] + [out[k]] + vals[j + 1:])
+            total, losses = _loss_terms(loss, inputs, targets)
+        backward(total, scaler)
+    optimizer_step(model, optimizer, scaler, args)
+    return losses
+
+
+def train_one_epoch(model, data, loss, epoch, optimizer, scaler, scheduler, args, tb_writer=None):
+    """Epoch loop with the reference's logging cadence (samples/s per GPU and whole job)."""
+    device = torch.device(args.device)
+    autocast = get_autocast(args.precision)
+    input_dtype = get_input_dtype(args.precision)
+    model.train()
+    data["train"].set_epoch(epoch)
+    dataloader = data["train"].dataloader
+    accum = getattr(args, "accum_freq", 1)
+    num_batches_per_epoch = dataloader.num_batches // accum
+    batch_time_m, data_time_m, losses_m = AverageMeter(), AverageMeter(), {}
+    pending = []
+    end = time.time()
+    for i, batch in enumerate(dataloader):
+        i_accum = i // accum
+        step = num_batches_per_epoch * epoch + i_accum
+        if scheduler is not None and not getattr(args, "skip_scheduler", False):
+            scheduler(step)
+        images, texts, targets = batch if len(batch) == 3 else (batch[0], None, batch[1])
+        images = images.to(device=device, dtype=input_dtype, non_blocking=True)
+        texts = texts.to(device=device, non_blocking=True) if texts is not None else None
+        targets = targets.to(device=device, non_blocking=True)
+        data_time_m.update(time.time() - end)
+        if accum == 1:
+            losses = train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast)
+        else:
+            pending.append((images, texts, targets))
+            if (i + 1) % accum:
+                continue
+            losses = train_step_accum(model, pending, loss, optimizer, scaler, args, autocast)
+            pending = []
+        batch_time_m.update(time.time() - end)
+        end = time.time()
+        batch_count = i_accum + 1
+        if is_master(args) and (i_accum % getattr(args, "log_every_n_steps", 100) == 0
+                                or batch_count == num_batches_per_epoch):
+            bs = len(images)
+            for k, v in losses.items():
+                losses_m.setdefault(k, AverageMeter()).update(v.item(), bs)
+            per_gpu = accum * bs / max(batch_time_m.val, 1e-9)
+            logging.info(
+                f"Train Epoch: {epoch} [{batch_count}/{num_batches_per_epoch}] "
+                f"Data (t): {data_time_m.avg:.3f} Batch (t): {batch_time_m.avg:.3f}, "
+                f"{per_gpu * args.world_size:#g}/s, {per_gpu:#g}/s/gpu "
+                f"LR: {optimizer.param_groups[0]['lr']:5f} "
+                + " ".join(f"{k}: {m.val:#.5g} ({m.avg:#.5g})" for k, m in losses_m.items()))
+            if tb_writer is not None:
+                tb_writer.add_scalar("train/samples_per_second", per_gpu * args.world_size, step)
+            batch_time_m.reset()
+            data_time_m.reset()
+    return {k: m.avg for k, m in losses_m.items()}

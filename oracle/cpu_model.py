@@ -1,0 +1,108 @@
+"""CPU restatement of the stage-1 training step (TEST / BASELINE INFRASTRUCTURE ONLY).
+
+Used by bench.py's `cpu_baseline` leg and by tests: the SAME module classes
+as the product (mamba_clip_amd.model), with their four HIP entry points
+swapped for the fp32 CPU restatements of this directory while the context is
+active, and the loss computed by oracle/loss_ref.clip_loss (loss.py:89-147).
+This is the "reference's CPU path" of SURVEY.md 8(d): fp32 PyTorch-CPU eager,
+scan by the model.py:83-169 semantics.  The product path never imports this.
+"""
+import time
+from contextlib import contextmanager
+
+import torch
+import torch.nn.functional as F
+
+from .loss_ref import clip_loss
+from .scan_ref import selective_scan_ref
+
+
+def _add_rmsnorm_f32(x, res, w, eps=1e-5):
+    h = x.float() + (res.float() if res is not None else 0)
+    y = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype), h
+
+
+def _causal_conv1d_f32(x, w, b=None, silu=True):
+    D, K = w.shape[0], w.shape[-1]
+    y = F.conv1d(x, w.reshape(D, 1, K).to(x.dtype), b.to(x.dtype) if b is not None else None,
+                 padding=K - 1, groups=D)[..., : x.shape[-1]]
+    return F.silu(y) if silu else y
+
+
+def _im2col(img, P):
+    B, C, H, W = img.shape
+    return F.unfold(img, P, stride=P).transpose(1, 2).reshape(B * (H // P) * (W // P), C * P * P)
+
+
+_OPS = {"selective_scan_fn": selective_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
+        "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col}
+
+
+@contextmanager
+def oracle_ops():
+    """Temporarily route mamba_clip_amd.model's op references to the CPU restatements."""
+    import mamba_clip_amd.model as M
+    saved = {k: getattr(M, k) for k in _OPS}
+    try:
+        for k, f in _OPS.items():
+            setattr(M, k, f)
+        yield
+    finally:
+        for k, f in saved.items():
+            setattr(M, k, f)
+
+
+def oracle_clip_loss(image_features, text_features, logit_scale, output_dict=True, target=None, **_):
+    loss = clip_loss(image_features, text_features, logit_scale)
+    return {"contrastive_loss": loss} if output_dict else loss
+
+
+def cpu_train_pairs_per_sec(model_name="vit_b16-mamba130m", batch=8, steps=2, warmup=1, threads=None, seed=0):
+    """fp32 CPU fwd+bwd+AdamW steps of the same architecture; returns (pairs/s, seconds timed)."""
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.model import build_clip
+    if threads:
+        torch.set_num_threads(threads)
+    torch.manual_seed(seed)
+    model = build_clip(model_name)
+    text = model.text
+    images, texts, _ = synthetic_batch(batch, 224 if model_name != "tiny-mamba-clip" else 32,
+                                       text.context_length, text.vocab_size, seed=1000)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-5)
+    with oracle_ops():
+        def step():
+            opt.zero_grad(set_to_none=True)
+            out = model(images, texts)
+            oracle_clip_loss(**out)["contrastive_loss"].backward()
+            opt.step()
+            with torch.no_grad():
+                model.logit_scale.clamp_(0, 4.605170185988092)
+        for _ in range(warmup):
+            step()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = time.perf_counter() - t0
+    return batch * steps / dt, dt
+
+
+def cpu_scan_gbps(batch=1, dim=3072, seqlen=4096, dstate=16, threads=None, seed=0):
+    """Oracle selective-scan forward at C4 channel/length shape, bf16 I/O semantics; returns (GB/s, seconds)."""
+    if threads:
+        torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randn(batch, dim, seqlen, generator=g).bfloat16()
+    dl = (torch.randn(batch, dim, seqlen, generator=g) * 0.5).bfloat16()
+    z = torch.randn(batch, dim, seqlen, generator=g).bfloat16()
+    A = -torch.exp(torch.log(torch.arange(1, dstate + 1).float()).repeat(dim, 1))
+    B = torch.randn(batch, dstate, seqlen, generator=g).bfloat16()
+    C = torch.randn(batch, dstate, seqlen, generator=g).bfloat16()
+    Dv = torch.ones(dim)
+    bias = torch.full((dim,), -3.0)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        selective_scan_ref(u, dl, A, B, C, Dv, z=z, delta_bias=bias, delta_softplus=True)
+    dt = time.perf_counter() - t0
+    nbytes = batch * dim * seqlen * 8 + 2 * batch * dstate * seqlen * 2 + (dim * dstate + 2 * dim) * 4
+    return nbytes / dt / 1e9, dt
