@@ -43,17 +43,19 @@ int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy
 size_t mc_add_rmsnorm_bwd_workspace_bytes(int32_t rows, int32_t cols);
 
 /* y[b, d, t] = act( bias[d] + sum_k w[d, k] * x[b, d, t - (K-1) + k] ), zero left padding.
- * x: (batch, dim, seqlen) with strides (x_bs, x_ds, 1); y contiguous; w (dim, K) fp32,
- * bias (dim,) fp32 nullable; act = SiLU if silu else identity.  K <= 8. */
+ * x, y: (batch, dim, seqlen) with strides (x_bs, x_ds, 1) / (y_bs, y_ds, 1) -- e.g. the
+ * channel-major (dim, batch*seqlen) GEMM output viewed as (batch, dim, seqlen);
+ * w (dim, K) fp32, bias (dim,) fp32 nullable; act = SiLU if silu else identity.  K <= 8. */
 int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype, const void* x,
                          int64_t x_bs, int64_t x_ds, const float* w, const float* bias, int32_t silu, void* y,
-                         void* stream);
+                         int64_t y_bs, int64_t y_ds, void* stream);
 
-/* Backward: dx (contiguous, dtype), dw (dim, K) fp32, dbias (dim) fp32 (nullable). */
+/* Backward: dx (dtype, strides dx_bs, dx_ds, 1), dw (dim, K) fp32, dbias (dim) fp32 (nullable). */
 int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype, const void* x,
                          int64_t x_bs, int64_t x_ds, const float* w, const float* bias, int32_t silu, const void* dy,
-                         void* dx, float* dw, float* dbias, void* workspace, size_t workspace_bytes, void* stream);
-size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t K);
+                         int64_t dy_bs, int64_t dy_ds, void* dx, int64_t dx_bs, int64_t dx_ds, float* dw,
+                         float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t K);
 
 /* patches[(b*ph + i)*pw + j, (c*P + ky)*P + kx] = img[b, c, i*P + ky, j*P + kx]
  * img (batch, C, H, W) contiguous; H % P == W % P == 0; same dtype in and out. */

@@ -90,6 +90,11 @@ typedef struct mc_scan_bwd_params {
   int64_t delta_batch_stride, delta_dim_stride;
   int64_t z_batch_stride, z_dim_stride;
   int64_t dout_batch_stride, dout_dim_stride;
+  /* output strides of du / ddelta / dz (seqlen stride 1): a caller keeping
+   * activations channel-major passes the strides of u / delta / z */
+  int64_t du_batch_stride, du_dim_stride;
+  int64_t ddelta_batch_stride, ddelta_dim_stride;
+  int64_t dz_batch_stride, dz_dim_stride;
   int64_t B_batch_stride, B_group_stride, B_dstate_stride;
   int64_t C_batch_stride, C_group_stride, C_dstate_stride;
   const void* u;
@@ -102,7 +107,7 @@ typedef struct mc_scan_bwd_params {
   const float* delta_bias;    /* nullable */
   const void* dout;           /* gradient of out (itype) */
   const float* chunk_states;  /* REQUIRED: produced by mc_scan_fwd on the same inputs */
-  /* outputs: du/ddelta/dz contiguous (batch, dim, seqlen) in itype; dB/dC
+  /* outputs: du/ddelta/dz (batch, dim, seqlen) in itype with the strides above; dB/dC
    * contiguous (batch, n_groups, dstate, seqlen) in wtype; dA (dim, dstate),
    * dD (dim,), ddelta_bias (dim,) fp32.  dz / dD / ddelta_bias nullable when
    * the corresponding input is absent. */

@@ -165,105 +165,199 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ i
 constexpr int kNormGrid = 256;  // blocks of 4 waves: 1024 waves -> 1024 dw partial rows
 
 // ------------------------------------------------------------------ causal conv1d
-// One thread per (b, d) row: sliding window over the sequence in registers;
-// per-row dw/dbias partials in the backward.
+// Vector tiles along the sequence: each work item owns VEC consecutive
+// positions t0 .. t0+VEC-1 of one (b, d) row (one 16-B load), and reads the
+// K-1 positions before it from the neighbouring vector(s) (cache hits), so
+// the row is streamed once, coalesced along L.  VEC = 1 is the generic path
+// for unaligned strides / ragged L.
 constexpr int kMaxK = 8;
 
-template <typename T>
-__global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
-                                                         int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
-                                                         const float* __restrict__ bias, int silu,
-                                                         T* __restrict__ y) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= (int64_t)batch * dim) return;
-  const int b = (int)(row / dim), d = (int)(row % dim);
-  const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
-  T* yr = y + row * L;
-  float wk[kMaxK], win[kMaxK];
+template <typename T, int VEC>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, float (&v)[VEC]) {
+  if constexpr (VEC == 1) {
+    v[0] = to_f(*p);
+  } else {
+    const uint4 q = ld16(p);
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) { wk[k] = k < K ? w[d * K + k] : 0.f; win[k] = 0.f; }
-  const float bv = bias ? bias[d] : 0.f;
-  for (int t = 0; t < L; ++t) {
-#pragma unroll
-    for (int k = 0; k < kMaxK - 1; ++k) win[k] = win[k + 1];
-    win[kMaxK - 1] = to_f(xr[t]);
-    float acc = bv;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-      if (k < K) acc = fmaf(wk[k], win[kMaxK - K + k], acc);
-    yr[t] = from_f<T>(silu ? silu_f(acc) : acc);
+    for (int e = 0; e < VEC; ++e) v[e] = elem_f<T>(q, e);
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+template <typename T, int VEC>
+__device__ __forceinline__ void store_vec(T* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 1) {
+    *p = from_f<T>(v[0]);
+  } else {
+    st16(p, pack_f<T>(v));
+  }
+}
+
+// Window of x[t0 - NP*VEC .. t0 + (1+NN)*VEC - 1] in registers (zero outside [0, L)).
+template <typename T, int VEC, int NP, int NN>
+__device__ __forceinline__ void load_window(const T* __restrict__ xr, int t0, int L,
+                                            float (&win)[(NP + 1 + NN) * VEC]) {
+#pragma unroll
+  for (int j = -NP; j <= NN; ++j) {
+    const int t = t0 + j * VEC;
+    float v[VEC];
+    if (t >= 0 && t < L) {
+      load_vec<T, VEC>(xr + t, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) win[(j + NP) * VEC + e] = v[e];
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
                                                          int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int silu,
-                                                         const T* __restrict__ dy, T* __restrict__ dx,
-                                                         float* __restrict__ part) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= (int64_t)batch * dim) return;
-  const int b = (int)(row / dim), d = (int)(row % dim);
+                                                         T* __restrict__ y, int64_t y_bs, int64_t y_ds) {
+  constexpr int NP = (kMaxK - 1 + VEC - 1) / VEC;   // previous vectors covering the K-1 halo
+  const int nchunk = (L + VEC - 1) / VEC;
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= (int64_t)batch * dim * nchunk) return;
+  const int64_t row = item / nchunk;
+  const int t0 = (int)(item - row * nchunk) * VEC;
+  const int b = (int)(row / dim), d = (int)(row - (int64_t)b * dim);
   const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
-  const T* gr = dy + row * L;
-  T* dxr = dx + row * L;
+  float win[(NP + 1) * VEC];
+  load_window<T, VEC, NP, 0>(xr, t0, L, win);
   float wk[kMaxK];
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
   const float bv = bias ? bias[d] : 0.f;
-  // reverse walk: dpre window holds dpre[t .. t+K-1]; x window x[t-K+1 .. t]
-  float dwk[kMaxK], db = 0.f, dp[kMaxK];
+  float out[VEC];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) { dwk[k] = 0.f; dp[k] = 0.f; }
-  for (int t = L - 1; t >= 0; --t) {
-    // pre-activation at t (recomputed) and its gradient
-    float xw[kMaxK];
+  for (int i = 0; i < VEC; ++i) {
+    float acc = bv;
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k) {
-      const int tt = t - (K - 1) + k;
-      xw[k] = (k < K && tt >= 0) ? to_f(xr[tt]) : 0.f;
-    }
-    float pre = bv;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-      if (k < K) pre = fmaf(wk[k], xw[k], pre);
-    float g = to_f(gr[t]);
-    if (silu) {
-      const float s = sigmoid_f(pre);
-      g *= s * (1.f + pre * (1.f - s));
-    }
-    // shift: dp[k] = dpre[t + k]
-#pragma unroll
-    for (int k = kMaxK - 1; k > 0; --k) dp[k] = dp[k - 1];
-    dp[0] = g;
-    db += g;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-      if (k < K) dwk[k] = fmaf(g, xw[k], dwk[k]);
-    // dx[t] = sum_k w[k] * dpre[t + (K-1) - k]
-    float gx = 0.f;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-      if (k < K && t + (K - 1) - k < L) gx = fmaf(wk[k], dp[K - 1 - k], gx);
-    dxr[t] = from_f<T>(gx);
+    for (int k = 0; k < kMaxK; ++k)   // tap k reads position t0 + i - (K-1) + k
+      if (k < K) acc = fmaf(wk[k], win[NP * VEC + i - (K - 1) + k], acc);
+    out[i] = silu ? silu_f(acc) : acc;
   }
-  float* pr = part + row * (kMaxK + 1);
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) pr[k] = dwk[k];
-  pr[kMaxK] = db;
+  store_vec<T, VEC>(y + (int64_t)b * y_bs + (int64_t)d * y_ds + t0, out);
 }
 
-// dw[d, k] = sum_b part[b, d, k]; dbias[d] = sum_b part[b, d, K]
-__global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restrict__ part, int batch, int dim, int K,
+// Backward.  One wave per (channel d, slice of the channel's batch x chunk
+// items): per item it recomputes the pre-activation over t0 .. t0+VEC+K-2,
+// forms g = dy * act'(pre), writes dx for its VEC positions and accumulates
+// dw / dbias in registers; a wave reduction then writes one partial per
+// (slice, d) -- deterministic, no atomics.
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+                                                         int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int silu,
+                                                         const T* __restrict__ dy, int64_t dy_bs, int64_t dy_ds,
+                                                         T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
+                                                         int items_per_slice, float* __restrict__ part) {
+  constexpr int NP = (kMaxK - 1 + VEC - 1) / VEC;
+  constexpr int NN = NP;                             // following vectors covering t0+VEC .. t0+VEC+K-2
+  constexpr int W = (NP + 1 + NN) * VEC;
+  constexpr int G = VEC + kMaxK - 1;                 // g positions t0 .. t0+VEC+K-2
+  const int lane = threadIdx.x & 63;
+  const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= dim) return;
+  const int slice = blockIdx.y;
+  const int nchunk = (L + VEC - 1) / VEC;
+  const int total = batch * nchunk;
+  const int i_begin = slice * items_per_slice;
+  const int i_end = min(total, i_begin + items_per_slice);
+  float wk[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
+  const float bv = bias ? bias[d] : 0.f;
+  float dwk[kMaxK], db = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) dwk[k] = 0.f;
+  for (int item = i_begin + lane; item < i_end; item += 64) {
+    const int b = item / nchunk;
+    const int t0 = (item - b * nchunk) * VEC;
+    const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
+    const T* gyr = dy + (int64_t)b * dy_bs + (int64_t)d * dy_ds;
+    T* dxr = dx + (int64_t)b * dx_bs + (int64_t)d * dx_ds;
+    float win[W];
+    load_window<T, VEC, NP, NN>(xr, t0, L, win);
+    float gy[(1 + NN) * VEC];
+#pragma unroll
+    for (int j = 0; j <= NN; ++j) {
+      const int t = t0 + j * VEC;
+      float v[VEC];
+      if (t < L) {
+        load_vec<T, VEC>(gyr + t, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) gy[j * VEC + e] = v[e];
+    }
+    float g[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      float pre = bv;
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k)
+        if (k < K) pre = fmaf(wk[k], win[NP * VEC + j - (K - 1) + k], pre);
+      float gj = gy[j];                               // zero beyond L (loaded as 0)
+      if (silu) {
+        const float s = sigmoid_f(pre);
+        gj *= s * (1.f + pre * (1.f - s));
+      }
+      g[j] = (t0 + j < L) ? gj : 0.f;
+    }
+    float out[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k)               // dx[t] = sum_k w[k] g[t + K-1-k]
+        if (k < K) acc = fmaf(wk[k], g[i + (K - 1) - k], acc);
+      out[i] = acc;
+      db += g[i];
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k)
+        if (k < K) dwk[k] = fmaf(g[i], win[NP * VEC + i - (K - 1) + k], dwk[k]);
+    }
+    store_vec<T, VEC>(dxr + t0, out);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) dwk[k] += __shfl_xor(dwk[k], o);
+    db += __shfl_xor(db, o);
+  }
+  if (lane == 0) {
+    float* pr = part + ((int64_t)slice * dim + d) * (kMaxK + 1);
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) pr[k] = dwk[k];
+    pr[kMaxK] = db;
+  }
+}
+
+// dw[d, k] = sum_s part[s, d, k]; dbias[d] = sum_s part[s, d, kMaxK]   (fixed order)
+__global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restrict__ part, int nslice, int dim, int K,
                                                             float* __restrict__ dw, float* __restrict__ dbias) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= dim * (K + 1)) return;
   const int d = i / (K + 1), k = i % (K + 1);
   const int slot = k < K ? k : kMaxK;
   float s = 0.f;
-  for (int b = 0; b < batch; ++b) s += part[((int64_t)b * dim + d) * (kMaxK + 1) + slot];
+  for (int b = 0; b < nslice; ++b) s += part[((int64_t)b * dim + d) * (kMaxK + 1) + slot];
   if (k < K) dw[d * K + k] = s;
   else if (dbias) dbias[d] = s;
+}
+
+// batch x chunk items per backward wave: ~8 items per lane
+static inline int conv1d_items_per_slice(int batch, int L, int vec) {
+  const int nchunk = (L + vec - 1) / vec;
+  const int total = batch * nchunk;
+  const int target = 64 * 8;
+  const int nslice = std::max(1, (total + target - 1) / target);
+  return (total + nslice - 1) / nslice;
 }
 
 // ------------------------------------------------------------------ patch im2col
@@ -340,29 +434,49 @@ extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, con
   return check_launch("mc_add_rmsnorm_bwd");
 }
 
+// VEC path when every row start is 16-B aligned and L is a whole number of vectors.
+static bool conv1d_vec_ok(const void* p, int64_t bs, int64_t ds, int V) {
+  return aligned16(p) && bs % V == 0 && ds % V == 0;
+}
+
+#define MC_DISPATCH_VEC(vec, ...)                                      \
+  do {                                                                 \
+    if ((vec) == 1) { constexpr int VEC = 1; __VA_ARGS__; }            \
+    else if ((vec) == 4) { constexpr int VEC = 4; __VA_ARGS__; }       \
+    else { constexpr int VEC = 8; __VA_ARGS__; }                       \
+  } while (0)
+
 extern "C" int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype,
                                     const void* x, int64_t x_bs, int64_t x_ds, const float* w, const float* bias,
-                                    int32_t silu, void* y, void* stream) {
+                                    int32_t silu, void* y, int64_t y_bs, int64_t y_ds, void* stream) {
   MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_causal_conv1d_fwd: bad dtype");
   MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0 && K >= 1 && K <= kMaxK, MC_ERR_SHAPE,
            "mc_causal_conv1d_fwd: bad shape (K must be in [1, %d])", kMaxK);
   if (batch == 0 || seqlen == 0) return MC_OK;
   MC_CHECK(x && w && y, MC_ERR_INVALID, "mc_causal_conv1d_fwd: x, w, y required");
-  const int64_t rows = (int64_t)batch * dim;
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((conv1d_fwd_kernel<T>), dim3((rows + 255) / 256), dim3(256), 0,
-                                          (hipStream_t)stream, batch, dim, seqlen, K, (const T*)x, x_bs, x_ds, w, bias,
-                                          silu, (T*)y));
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  const int vec = seqlen % V == 0 && conv1d_vec_ok(x, x_bs, x_ds, V) && conv1d_vec_ok(y, y_bs, y_ds, V) ? V : 1;
+  const int64_t items = (int64_t)batch * dim * ((seqlen + vec - 1) / vec);
+  const dim3 grid((unsigned)((items + 255) / 256));
+  MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
+    hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen, K,
+                       (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
+  }));
   return check_launch("mc_causal_conv1d_fwd");
 }
 
-extern "C" size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t K) {
+extern "C" size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t K) {
   (void)K;
-  return (size_t)batch * dim * (kMaxK + 1) * sizeof(float);
+  const int items = conv1d_items_per_slice(batch, seqlen, 1);          // VEC = 1 has the most slices
+  const int64_t total = (int64_t)batch * std::max(seqlen, 1);
+  const int64_t nslice = std::max<int64_t>(1, (total + items - 1) / items);
+  return (size_t)nslice * dim * (kMaxK + 1) * sizeof(float);
 }
 
 extern "C" int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, int32_t K, int32_t dtype,
                                     const void* x, int64_t x_bs, int64_t x_ds, const float* w, const float* bias,
-                                    int32_t silu, const void* dy, void* dx, float* dw, float* dbias, void* workspace,
+                                    int32_t silu, const void* dy, int64_t dy_bs, int64_t dy_ds, void* dx,
+                                    int64_t dx_bs, int64_t dx_ds, float* dw, float* dbias, void* workspace,
                                     size_t workspace_bytes, void* stream) {
   MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_causal_conv1d_bwd: bad dtype");
   MC_CHECK(batch >= 0 && dim > 0 && seqlen >= 0 && K >= 1 && K <= kMaxK, MC_ERR_SHAPE, "mc_causal_conv1d_bwd: bad shape");
@@ -373,15 +487,22 @@ extern "C" int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, 
     return MC_OK;
   }
   MC_CHECK(x && w && dy && dx && dw, MC_ERR_INVALID, "mc_causal_conv1d_bwd: x, w, dy, dx, dw required");
-  MC_CHECK(workspace && workspace_bytes >= mc_causal_conv1d_bwd_workspace_bytes(batch, dim, K), MC_ERR_WORKSPACE,
-           "mc_causal_conv1d_bwd: workspace too small");
+  MC_CHECK(workspace && workspace_bytes >= mc_causal_conv1d_bwd_workspace_bytes(batch, dim, seqlen, K),
+           MC_ERR_WORKSPACE, "mc_causal_conv1d_bwd: workspace too small");
   float* part = reinterpret_cast<float*>(workspace);
-  const int64_t rows = (int64_t)batch * dim;
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((conv1d_bwd_kernel<T>), dim3((rows + 255) / 256), dim3(256), 0, s, batch,
-                                          dim, seqlen, K, (const T*)x, x_bs, x_ds, w, bias, silu, (const T*)dy,
-                                          (T*)dx, part));
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  const int vec = seqlen % V == 0 && conv1d_vec_ok(x, x_bs, x_ds, V) && conv1d_vec_ok(dy, dy_bs, dy_ds, V) &&
+                          conv1d_vec_ok(dx, dx_bs, dx_ds, V) ? V : 1;
+  const int per = conv1d_items_per_slice(batch, seqlen, vec);
+  const int total = batch * ((seqlen + vec - 1) / vec);
+  const int nslice = (total + per - 1) / per;
+  const dim3 grid((unsigned)((dim + 3) / 4), (unsigned)nslice);
+  MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
+    hipLaunchKernelGGL((conv1d_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, batch, dim, seqlen, K, (const T*)x, x_bs,
+                       x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
+  }));
   const int n = dim * (K + 1);
-  hipLaunchKernelGGL(conv1d_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, batch, dim, K, dw, dbias);
+  hipLaunchKernelGGL(conv1d_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, nslice, dim, K, dw, dbias);
   return check_launch("mc_causal_conv1d_bwd");
 }
 

@@ -34,10 +34,11 @@ constexpr int kTB = kS;  // positions per backward tile (== saved-state granular
 struct BwdArgs {
   int batch, dim, seqlen, dstate, n_groups, n_states, nblk, total_blocks, softplus;
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, go_bs, go_ds;
+  int64_t du_bs, du_ds, ddt_bs, ddt_ds, dz_bs, dz_ds;  // output strides (seqlen stride 1)
   const void* u; const void* delta; const void* z; const void* dout;
   const float* A; const float* bct; const float* D; const float* delta_bias;
   const float* chunk_states;
-  void* du; void* ddelta; void* dz;  // contiguous (batch, dim, seqlen)
+  void* du; void* ddelta; void* dz;
   float* slab_bc;                    // [b*G+g][nblk][kN][2][seqlen]
   float* slab_a;                     // [b][dim][kN]
   float* slab_d;                     // [b][dim]
@@ -335,14 +336,17 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
       const int col0 = l0 + c * VI;
       const int nv = max(0, min(VI, L_ - col0));
       const float* src = reinterpret_cast<const float*>(rowbuf + r * RW::kStride);
-      const int64_t off = ((int64_t)b * a.dim + dbase + r) * L_ + col0;   // outputs are contiguous
+      const int64_t dd = dbase + r;
 #pragma unroll
       for (int which = 0; which < 3; ++which) {
         if (which == 2 && !hasZ) continue;
         float v[VI];
 #pragma unroll
         for (int e = 0; e < VI; ++e) v[e] = src[which * kTB + c * VI + e];
-        TI* dst = reinterpret_cast<TI*>(which == 0 ? a.du : (which == 1 ? a.ddelta : a.dz)) + off;
+        const int64_t off = which == 0   ? (int64_t)b * a.du_bs + dd * a.du_ds
+                            : which == 1 ? (int64_t)b * a.ddt_bs + dd * a.ddt_ds
+                                         : (int64_t)b * a.dz_bs + dd * a.dz_ds;
+        TI* dst = reinterpret_cast<TI*>(which == 0 ? a.du : (which == 1 ? a.ddelta : a.dz)) + off + col0;
         const uint4 q = pack_f<TI>(v);
         if (full) st16(dst, q);
         else st16_masked(dst, q, nv);
@@ -521,6 +525,9 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   a.A = p->A; a.bct = reinterpret_cast<const float*>(ws + w.bct); a.D = p->D; a.delta_bias = p->delta_bias;
   a.chunk_states = p->chunk_states;
   a.du = p->du; a.ddelta = p->ddelta; a.dz = p->dz;
+  a.du_bs = p->du_batch_stride; a.du_ds = p->du_dim_stride;
+  a.ddt_bs = p->ddelta_batch_stride; a.ddt_ds = p->ddelta_dim_stride;
+  a.dz_bs = p->dz_batch_stride; a.dz_ds = p->dz_dim_stride;
   a.slab_bc = reinterpret_cast<float*>(ws + w.slab_bc);
   a.slab_a = reinterpret_cast<float*>(ws + w.slab_a);
   a.slab_d = reinterpret_cast<float*>(ws + w.slab_d);
@@ -533,9 +540,9 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
                        vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
                        vec_ok(p->dout, p->dout_batch_stride, p->dout_dim_stride, 0, ib) &&
-                       vec_ok(p->du, (int64_t)p->dim * p->seqlen, p->seqlen, 0, ib) &&
-                       vec_ok(p->ddelta, (int64_t)p->dim * p->seqlen, p->seqlen, 0, ib) &&
-                       vec_ok(p->dz, (int64_t)p->dim * p->seqlen, p->seqlen, 0, ib);
+                       vec_ok(p->du, p->du_batch_stride, p->du_dim_stride, 0, ib) &&
+                       vec_ok(p->ddelta, p->ddelta_batch_stride, p->ddelta_dim_stride, 0, ib) &&
+                       vec_ok(p->dz, p->dz_batch_stride, p->dz_dim_stride, 0, ib);
   if (p->itype == MC_DTYPE_F32) rc = launch_bwd_t<float>(a, aligned, s);
   else if (p->itype == MC_DTYPE_BF16) rc = launch_bwd_t<bf16_t>(a, aligned, s);
   else rc = launch_bwd_t<f16_t>(a, aligned, s);

@@ -45,6 +45,9 @@ class ScanBwdParams(ctypes.Structure):
         ("delta_batch_stride", c_i64), ("delta_dim_stride", c_i64),
         ("z_batch_stride", c_i64), ("z_dim_stride", c_i64),
         ("dout_batch_stride", c_i64), ("dout_dim_stride", c_i64),
+        ("du_batch_stride", c_i64), ("du_dim_stride", c_i64),
+        ("ddelta_batch_stride", c_i64), ("ddelta_dim_stride", c_i64),
+        ("dz_batch_stride", c_i64), ("dz_dim_stride", c_i64),
         ("B_batch_stride", c_i64), ("B_group_stride", c_i64), ("B_dstate_stride", c_i64),
         ("C_batch_stride", c_i64), ("C_group_stride", c_i64), ("C_dstate_stride", c_i64),
         ("u", c_vp), ("delta", c_vp), ("A", c_fp), ("B", c_vp), ("C", c_vp),
@@ -87,10 +90,11 @@ SYMBOLS = {
                                           ctypes.c_size_t, c_vp]),
     "mc_add_rmsnorm_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "mc_causal_conv1d_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_i64, c_fp, c_fp, c_i32,
-                                            c_vp, c_vp]),
+                                            c_vp, c_i64, c_i64, c_vp]),
     "mc_causal_conv1d_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_i64, c_fp, c_fp, c_i32,
-                                            c_vp, c_vp, c_fp, c_fp, c_vp, ctypes.c_size_t, c_vp]),
-    "mc_causal_conv1d_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+                                            c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_fp, c_fp, c_vp,
+                                            ctypes.c_size_t, c_vp]),
+    "mc_causal_conv1d_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_patch_im2col": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
 }
 

@@ -42,8 +42,12 @@ def _dt_bias_init(d_inner, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
 class MambaMixer(nn.Module):
     """One Mamba mixer: in_proj -> causal conv1d+SiLU -> x_proj/dt_proj -> selective scan (z-gated) -> out_proj.
 
-    Activations stay (batch, channels, seqlen) between the GEMMs so the conv
-    and the scan read unit-stride rows (no transposes on the hot path).
+    Channel-major activations: every projection is ONE 2-D GEMM on the
+    (channels, batch*seqlen) matrix, and the conv / scan see it as a
+    (batch, channels, seqlen) view with strides (seqlen, batch*seqlen, 1) --
+    unit stride along the sequence, no transposes or copies between the GEMMs
+    (the HIP kernels take batch/channel strides and write outputs and
+    gradients in the same layout).
     """
 
     def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto"):
@@ -66,22 +70,27 @@ class MambaMixer(nn.Module):
         self.D._no_weight_decay = True
         self.out_proj = nn.Linear(self.d_inner, d_model, bias=False)
 
-    def forward(self, hidden):  # (B, L, d_model)
-        Bsz, L, _ = hidden.shape
+    def forward(self, hidden):  # (B, L, d_model) contiguous
+        Bsz, L, dm = hidden.shape
         dt_in = hidden.dtype
-        w_in = self.in_proj.weight.to(dt_in)
-        xz = torch.matmul(w_in, hidden.transpose(1, 2))                      # (B, 2*d_inner, L)
-        x, z = xz[:, : self.d_inner], xz[:, self.d_inner:]
-        x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True)   # (B, d_inner, L)
-        x_dbl = torch.matmul(self.x_proj.weight.to(dt_in), x)                 # (B, R + 2N, L)
-        dt_raw = x_dbl[:, : self.dt_rank]
-        Bm = x_dbl[:, self.dt_rank: self.dt_rank + self.d_state]
-        Cm = x_dbl[:, self.dt_rank + self.d_state:]
-        delta = torch.matmul(self.dt_proj.weight.to(dt_in), dt_raw)          # (B, d_inner, L)
+        di, R, N = self.d_inner, self.dt_rank, self.d_state
+        H = hidden.reshape(Bsz * L, dm)
+        xz = torch.mm(self.in_proj.weight.to(dt_in), H.t())                  # (2*di, B*L)
+        x, z = xz.split(di, dim=0)
+        x = x.view(di, Bsz, L).transpose(0, 1)                                # (B, di, L) channel-major
+        z = z.view(di, Bsz, L).transpose(0, 1)
+        x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True)
+        x_dbl = torch.mm(self.x_proj.weight.to(dt_in), x.transpose(0, 1).reshape(di, Bsz * L))   # (R+2N, B*L)
+        dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
+        delta = torch.mm(self.dt_proj.weight.to(dt_in), dt_raw).view(di, Bsz, L).transpose(0, 1)
+        Bm = Bm.view(N, Bsz, L).transpose(0, 1)                               # (B, N, L)
+        Cm = Cm.view(N, Bsz, L).transpose(0, 1)
         A = -torch.exp(self.A_log.float())
         y = selective_scan_fn(x, delta, A, Bm, Cm, self.D.float(), z=z,
                               delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
-        return torch.matmul(y.transpose(1, 2), self.out_proj.weight.to(dt_in).t())   # (B, L, d_model)
+        y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
+        out = torch.mm(y2.t(), self.out_proj.weight.to(dt_in).t())             # (B*L, d_model)
+        return out.view(Bsz, L, dm)
 
 
 class MambaLayer(nn.Module):

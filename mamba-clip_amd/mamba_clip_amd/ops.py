@@ -173,10 +173,11 @@ class CausalConv1dFn(torch.autograd.Function):
         K = weight.shape[-1]
         w = weight.reshape(D, K).float().contiguous()
         b = bias.float().contiguous() if bias is not None else None
-        y = torch.empty(Bsz, D, L, device=x.device, dtype=x.dtype)
+        y = torch.empty_like(x)          # keeps a dense channel-major layout of x
         _lib.check(lib.mc_causal_conv1d_fwd(Bsz, D, L, K, _lib.dtype_code(x.dtype), x.data_ptr(), x.stride(0),
                                             x.stride(1), w.data_ptr(), _lib.ptr(b), int(silu), y.data_ptr(),
-                                            _lib.stream_handle(x.device)), "mc_causal_conv1d_fwd")
+                                            y.stride(0), y.stride(1), _lib.stream_handle(x.device)),
+                   "mc_causal_conv1d_fwd")
         ctx.save_for_backward(x, w, b if b is not None else w)
         ctx.meta = (silu, bias is not None, weight.shape, weight.dtype)
         return y
@@ -188,15 +189,18 @@ class CausalConv1dFn(torch.autograd.Function):
         silu, has_b, wshape, wdt = ctx.meta
         Bsz, D, L = x.shape
         K = w.shape[-1]
-        dy = dy.to(x.dtype).contiguous()
-        dx = torch.empty(Bsz, D, L, device=x.device, dtype=x.dtype)
+        dy = dy.to(x.dtype)
+        if dy.stride(-1) != 1:
+            dy = dy.contiguous()
+        dx = torch.empty_like(x)
         dw = torch.empty(D, K, device=x.device, dtype=torch.float32)
         db = torch.empty(D, device=x.device, dtype=torch.float32) if has_b else None
-        ws_b = lib.mc_causal_conv1d_bwd_workspace_bytes(Bsz, D, K)
+        ws_b = lib.mc_causal_conv1d_bwd_workspace_bytes(Bsz, D, L, K)
         ws = _ws(ws_b, x.device)
         _lib.check(lib.mc_causal_conv1d_bwd(Bsz, D, L, K, _lib.dtype_code(x.dtype), x.data_ptr(), x.stride(0),
                                             x.stride(1), w.data_ptr(), b.data_ptr() if has_b else None, int(silu),
-                                            dy.data_ptr(), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(),
+                                            dy.data_ptr(), dy.stride(0), dy.stride(1), dx.data_ptr(), dx.stride(0),
+                                            dx.stride(1), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(),
                                             ws_b, _lib.stream_handle(x.device)), "mc_causal_conv1d_bwd")
         return dx, dw.reshape(wshape).to(wdt), (db.to(wdt) if db is not None else None), None
 

@@ -62,7 +62,7 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     batch, dim, L = u.shape
     dstate = A.shape[1]
     G = B.shape[1]
-    out = torch.empty_like(u, memory_format=torch.contiguous_format)
+    out = torch.empty_like(u)      # same (dense) layout as u: channel-major callers stay channel-major
     nch = _lib.MC_SCAN_CHUNK and lib.mc_scan_n_chunks(L)
     states = (torch.empty(batch, dim, nch, dstate, device=u.device, dtype=torch.float32)
               if want_states else None)
@@ -96,10 +96,10 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
     batch, dim, L = u.shape
     dstate = A.shape[1]
     G = B.shape[1]
-    dout = dout.contiguous()
-    du = torch.empty_like(u, memory_format=torch.contiguous_format)
-    ddelta = torch.empty_like(delta, memory_format=torch.contiguous_format)
-    dz = torch.empty_like(z, memory_format=torch.contiguous_format) if z is not None else None
+    dout = _last_dim_contig(dout)
+    du = torch.empty_like(u)
+    ddelta = torch.empty_like(delta)
+    dz = torch.empty_like(z) if z is not None else None
     dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
     dC = torch.empty(C.shape, device=u.device, dtype=C.dtype)
     dA = torch.empty(dim, dstate, device=u.device, dtype=torch.float32)
@@ -116,6 +116,10 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
     if z is not None:
         p.z_batch_stride, p.z_dim_stride = z.stride(0), z.stride(1)
     p.dout_batch_stride, p.dout_dim_stride = dout.stride(0), dout.stride(1)
+    p.du_batch_stride, p.du_dim_stride = du.stride(0), du.stride(1)
+    p.ddelta_batch_stride, p.ddelta_dim_stride = ddelta.stride(0), ddelta.stride(1)
+    if dz is not None:
+        p.dz_batch_stride, p.dz_dim_stride = dz.stride(0), dz.stride(1)
     p.B_batch_stride, p.B_group_stride, p.B_dstate_stride = B.stride(0), B.stride(1), B.stride(2)
     p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
     p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()

@@ -65,6 +65,79 @@ def test_causal_conv1d_fwd_bwd():
             torch.testing.assert_close(bd.grad.cpu(), br.grad.float(), rtol=1e-3, atol=1e-3 * (B * L) ** 0.5)
 
 
+def test_causal_conv1d_channel_major_layout():
+    """x as the channel-major (dim, batch*L) GEMM output viewed (B, D, L): y / dx keep that layout."""
+    from mamba_clip_amd.ops import causal_conv1d
+    g = torch.Generator().manual_seed(2)
+    for dt in (torch.bfloat16, torch.float32):
+        for (B, D, L, K) in [(4, 96, 80, 4), (3, 16, 24, 8), (2, 24, 13, 4)]:
+            xz = torch.randn(2 * D, B * L, generator=g).to(dt)
+            w = torch.randn(D, 1, K, generator=g)
+            b = torch.randn(D, generator=g)
+            xd = xz.to(DEV).requires_grad_(True)
+            x = xd[:D].view(D, B, L).transpose(0, 1)
+            wd = w.to(DEV).requires_grad_(True)
+            bd = b.to(DEV).requires_grad_(True)
+            y = causal_conv1d(x, wd, bd, True)
+            assert y.stride() == x.stride()
+            gy = torch.randn(B, D, L, generator=g).to(dt)
+            y.backward(gy.to(DEV))
+            xr = xz[:D].view(D, B, L).transpose(0, 1).double().requires_grad_(True)
+            wr = w.double().requires_grad_(True)
+            br = b.double().requires_grad_(True)
+            yr = R.causal_conv1d_ref(xr, wr, br, True)
+            yr.backward(gy.double())
+            tol = 1e-5 if dt == torch.float32 else 2e-2
+            torch.testing.assert_close(y.float().cpu(), yr.float(), rtol=tol, atol=tol)
+            gx = xd.grad[:D].view(D, B, L).transpose(0, 1)
+            torch.testing.assert_close(gx.float().cpu(), xr.grad.float(), rtol=tol, atol=tol)
+            assert torch.count_nonzero(xd.grad[D:]) == 0
+            torch.testing.assert_close(wd.grad.cpu(), wr.grad.float(), rtol=1e-3, atol=1e-3 * (B * L) ** 0.5)
+            torch.testing.assert_close(bd.grad.cpu(), br.grad.float(), rtol=1e-3, atol=1e-3 * (B * L) ** 0.5)
+
+
+def test_scan_channel_major_layout():
+    """selective_scan_fn on channel-major views: out and du/ddelta/dz keep the input layout."""
+    from mamba_clip_amd.selective_scan_interface import selective_scan_fn
+    from oracle.scan_ref import selective_scan_ref
+    g = torch.Generator().manual_seed(3)
+    B, D, L, N = 3, 128, 48, 16
+    for dt in (torch.bfloat16, torch.float32):
+        big = torch.randn(3 * D, B * L, generator=g)
+        big[D:2 * D] *= 0.5
+        bc = torch.randn(2 * N, B * L, generator=g)
+        A = -torch.exp(torch.log(torch.arange(1, N + 1).float()).repeat(D, 1))
+        Dv = torch.randn(D, generator=g)
+        bias = torch.randn(D, generator=g) * 0.3 - 2.0
+
+        def views(t, tbc):
+            u, dl, z = (t[i * D:(i + 1) * D].view(D, B, L).transpose(0, 1) for i in range(3))
+            Bm, Cm = (tbc[i * N:(i + 1) * N].view(N, B, L).transpose(0, 1) for i in range(2))
+            return u, dl, z, Bm, Cm
+
+        bd = big.to(dt).to(DEV).requires_grad_(True)
+        bcd = bc.to(dt).to(DEV).requires_grad_(True)
+        u, dl, z, Bm, Cm = views(bd, bcd)
+        out = selective_scan_fn(u, dl, A.to(DEV), Bm, Cm, Dv.to(DEV), z=z, delta_bias=bias.to(DEV),
+                                delta_softplus=True)
+        assert out.stride() == u.stride()
+        dout = torch.randn(B, D, L, generator=g).to(dt)
+        out.backward(dout.to(DEV))
+        br = big.to(dt).double().requires_grad_(True)
+        bcr = bc.to(dt).double().requires_grad_(True)
+        ur, dlr, zr, Br, Cr = views(br, bcr)
+        ref = selective_scan_ref(ur, dlr, A.double(), Br, Cr, Dv.double(), z=zr, delta_bias=bias.double(),
+                                 delta_softplus=True, compute_dtype=torch.float64)
+        ref.backward(dout.double())
+        tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+        scale = ref.abs().max().item()
+        torch.testing.assert_close(out.double().cpu(), ref.to(dt).double(), rtol=tol, atol=tol * scale)
+        gs = br.grad.abs().max().item()
+        torch.testing.assert_close(bd.grad.double().cpu(), br.grad, rtol=tol, atol=tol * gs)
+        gs = bcr.grad.abs().max().item()
+        torch.testing.assert_close(bcd.grad.double().cpu(), bcr.grad, rtol=tol, atol=tol * gs)
+
+
 def test_patch_im2col_exact():
     from mamba_clip_amd.ops import patch_im2col
     img = torch.randn(2, 3, 32, 48)
