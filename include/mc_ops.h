@@ -6,6 +6,8 @@
  * Mamba block: SURVEY.md section 2.2); the build owns them:
  *   mc_add_rmsnorm_fwd/bwd  fused residual-add + RMSNorm (Mamba block pre-norm,
  *                           residual stream kept in fp32)
+ *   mc_add_layernorm_fwd/bwd fused residual-add + LayerNorm (ViT / BERT pre-LN
+ *                           blocks: timm Block norm1/norm2 + the residual add)
  *   mc_causal_conv1d_fwd/bwd depthwise causal conv1d (+ optional SiLU) over the
  *                           sequence of (batch, dim, seqlen) activations, the
  *                           short conv in front of the scan (the 2-D analogue is
@@ -41,6 +43,21 @@ int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy
                        const float* w, const float* rstd, void* dx, float* dres_in, float* dw, void* workspace,
                        size_t workspace_bytes, void* stream);
 size_t mc_add_rmsnorm_bwd_workspace_bytes(int32_t rows, int32_t cols);
+
+/* Residual-add + LayerNorm (ViT / BERT pre-LN blocks):
+ *   h = x + res (rounded to dtype; res nullable -> h = x), y = (h - mean) * rstd * w + bias.
+ * x, res, y, h_out: (rows, cols) row-major in dtype, 16-B aligned rows; w, bias (cols,) fp32
+ * (bias nullable); mean, rstd (rows,) fp32 saved for the backward.  h_out nullable.
+ * cols % 8 == 0 (16-bit) / % 4 (fp32) and <= 4096 / 2048. */
+int mc_add_layernorm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, const void* res, const float* w,
+                         const float* bias, float eps, void* y, void* h_out, float* mean, float* rstd, void* stream);
+
+/* Backward of (y, h) = add_layernorm(x, res): dx = dres = dh + d(LN)/dh . dy  (dh nullable),
+ * dw, dbias (cols,) fp32 (dbias nullable); deterministic reductions in workspace. */
+int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const void* dh, const void* h,
+                         const float* w, const float* mean, const float* rstd, void* dx, float* dw, float* dbias,
+                         void* workspace, size_t workspace_bytes, void* stream);
+size_t mc_add_layernorm_bwd_workspace_bytes(int32_t rows, int32_t cols);
 
 /* y[b, d, t] = act( bias[d] + sum_k w[d, k] * x[b, d, t - (K-1) + k] ), zero left padding.
  * x, y: (batch, dim, seqlen) with strides (x_bs, x_ds, 1) / (y_bs, y_ds, 1) -- e.g. the

@@ -1,6 +1,6 @@
 // ops.hip -- encoder kernels around the scan for MI355X (gfx950): fused
-// residual-add + RMSNorm, causal depthwise conv1d (+SiLU), patch im2col.
-// All three are HBM-bound streaming ops: 16-B vector accesses along the
+// residual-add + RMSNorm, residual-add + LayerNorm, causal depthwise conv1d
+// (+SiLU), patch im2col.  All are HBM-bound streaming ops: 16-B vector accesses along the
 // contiguous dimension, one pass over the data, fp32 math, deterministic
 // reductions (per-wave partial slabs + fixed-order column sums).
 #include <algorithm>
@@ -162,7 +162,180 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ i
   }
 }
 
+// out_y[c] = sum_r in[r * ld + y * cols + c] for y = blockIdx.y (0 -> out0, 1 -> out1), fixed order
+__global__ __launch_bounds__(256) void colsum_strided_kernel(const float* __restrict__ in, int nrows, int cols,
+                                                             int64_t ld, float* __restrict__ out0,
+                                                             float* __restrict__ out1) {
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  const float* base = in + (int64_t)blockIdx.y * cols;
+  float s = 0.f;
+  if (c < cols)
+    for (int r = q; r < nrows; r += 8) s += base[(int64_t)r * ld + c];
+  part[q][cx] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][cx];
+    (blockIdx.y == 0 ? out0 : out1)[c] = t;
+  }
+}
+
 constexpr int kNormGrid = 256;  // blocks of 4 waves: 1024 waves -> 1024 dw partial rows
+
+// ------------------------------------------------------------------ residual-add + LayerNorm
+// ViT/BERT pre-LN blocks: h = x + res (stored in the activation dtype, the
+// same rounding as the autocast residual add), y = (h - mean) * rstd * w + b
+// in fp32 math, stored in the activation dtype.  One wave per row, the row in
+// registers; the backward recomputes xhat from h and emits per-wave dw/db
+// partials reduced by colsum_kernel (deterministic).
+template <typename T>
+__global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int cols, const T* __restrict__ x,
+                                                                const T* __restrict__ res,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias, float eps,
+                                                                T* __restrict__ y, T* __restrict__ h_out,
+                                                                float* __restrict__ mean_out,
+                                                                float* __restrict__ rstd_out) {
+  constexpr int V = ElemTraits<T>::kVec;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int nvec = cols / V;
+  for (int row = wave; row < rows; row += nwaves) {
+    float h[kMaxVec][V];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        const uint4 q = ld16(x + off);
+        if (res) {
+          const uint4 r = ld16(res + off);
+          float hv[V];
+#pragma unroll
+          for (int e = 0; e < V; ++e) hv[e] = to_f(from_f<T>(elem_f<T>(q, e) + elem_f<T>(r, e)));
+          const uint4 hq = pack_f<T>(hv);
+          if (h_out) st16(h_out + off, hq);
+#pragma unroll
+          for (int e = 0; e < V; ++e) h[i][e] = hv[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(q, e);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) sum += h[i][e];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+    const float mu = sum / cols;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec)
+#pragma unroll
+        for (int e = 0; e < V; ++e) { const float c = h[i][e] - mu; ss = fmaf(c, c, ss); }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    const float rs = rsqrtf(ss / cols + eps);
+    if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        float o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          o[e] = fmaf((h[i][e] - mu) * rs, w[v * V + e], bias ? bias[v * V + e] : 0.f);
+        st16(y + (int64_t)row * cols + v * V, pack_f<T>(o));
+      }
+    }
+  }
+}
+
+// dh_total = dh + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+// dx (= dres) = dh_total;  part rows: [wave][0..cols) dw, [wave][cols..2cols) db
+template <typename T>
+__global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
+                                                                const T* __restrict__ dh,
+                                                                const T* __restrict__ hbuf,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                T* __restrict__ dx, float* __restrict__ part) {
+  constexpr int V = ElemTraits<T>::kVec;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int nvec = cols / V;
+  float dwacc[kMaxVec][V], dbacc[kMaxVec][V];
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i)
+#pragma unroll
+    for (int e = 0; e < V; ++e) { dwacc[i][e] = 0.f; dbacc[i][e] = 0.f; }
+  for (int row = wave; row < rows; row += nwaves) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[kMaxVec][V], g[kMaxVec][V];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        const uint4 q = ld16(dy + off);
+        const uint4 hq = ld16(hbuf + off);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float d = elem_f<T>(q, e);
+          xh[i][e] = (elem_f<T>(hq, e) - mu) * rs;
+          g[i][e] = d * w[v * V + e];
+          sg += g[i][e];
+          sgx = fmaf(g[i][e], xh[i][e], sgx);
+          dwacc[i][e] = fmaf(d, xh[i][e], dwacc[i][e]);
+          dbacc[i][e] += d;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      sg += __shfl_xor(sg, o);
+      sgx += __shfl_xor(sgx, o);
+    }
+    const float mg = sg / cols, mgx = sgx / cols;
+#pragma unroll
+    for (int i = 0; i < kMaxVec; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        float o[V];
+        uint4 dq = make_uint4(0u, 0u, 0u, 0u);
+        if (dh) dq = ld16(dh + off);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          o[e] = rs * (g[i][e] - mg - xh[i][e] * mgx);
+          if (dh) o[e] += elem_f<T>(dq, e);
+        }
+        st16(dx + off, pack_f<T>(o));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int v = lane + 64 * i;
+    if (v < nvec)
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        part[(int64_t)wave * 2 * cols + v * V + e] = dwacc[i][e];
+        part[(int64_t)wave * 2 * cols + cols + v * V + e] = dbacc[i][e];
+      }
+  }
+}
 
 // ------------------------------------------------------------------ causal conv1d
 // Vector tiles along the sequence: each work item owns VEC consecutive
@@ -432,6 +605,51 @@ extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, con
                                           (const T*)dy, dres, h, w, rstd, (T*)dx, dres_in, part));
   hipLaunchKernelGGL(colsum_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, kNormGrid * 4, cols, dw);
   return check_launch("mc_add_rmsnorm_bwd");
+}
+
+extern "C" int mc_add_layernorm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, const void* res,
+                                    const float* w, const float* bias, float eps, void* y, void* h_out, float* mean,
+                                    float* rstd, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_add_layernorm_fwd: bad dtype");
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0 && cols / V <= 64 * kMaxVec, MC_ERR_SHAPE,
+           "mc_add_layernorm_fwd: cols=%d must be a multiple of %d and <= %d", cols, V, 64 * kMaxVec * V);
+  if (rows == 0) return MC_OK;
+  MC_CHECK(x && w && y && mean && rstd && aligned16(x) && aligned16(y) && (!res || aligned16(res)) &&
+               (!h_out || aligned16(h_out)),
+           MC_ERR_INVALID, "mc_add_layernorm_fwd: x, w, y, mean, rstd required (16-B aligned rows)");
+  const int grid = std::min((rows + 3) / 4, 4096);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_layernorm_fwd_kernel<T>), dim3(grid), dim3(256), 0,
+                                          (hipStream_t)stream, rows, cols, (const T*)x, (const T*)res, w, bias, eps,
+                                          (T*)y, (T*)h_out, mean, rstd));
+  return check_launch("mc_add_layernorm_fwd");
+}
+
+extern "C" size_t mc_add_layernorm_bwd_workspace_bytes(int32_t rows, int32_t cols) {
+  (void)rows;
+  return (size_t)kNormGrid * 4 * 2 * cols * sizeof(float);
+}
+
+extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const void* dh,
+                                    const void* h, const float* w, const float* mean, const float* rstd, void* dx,
+                                    float* dw, float* dbias, void* workspace, size_t workspace_bytes, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_add_layernorm_bwd: bad dtype");
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0 && cols / V <= 64 * kMaxVec, MC_ERR_SHAPE,
+           "mc_add_layernorm_bwd: bad cols=%d", cols);
+  MC_CHECK(dy && h && w && mean && rstd && dx && dw, MC_ERR_INVALID,
+           "mc_add_layernorm_bwd: dy, h, w, mean, rstd, dx, dw required");
+  MC_CHECK(workspace && workspace_bytes >= mc_add_layernorm_bwd_workspace_bytes(rows, cols), MC_ERR_WORKSPACE,
+           "mc_add_layernorm_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(workspace);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_layernorm_bwd_kernel<T>), dim3(kNormGrid), dim3(256), 0, s, rows,
+                                          cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
+                                          part));
+  // part is [wave][2 * cols]: dw in columns [0, cols), dbias in [cols, 2 cols)
+  hipLaunchKernelGGL(colsum_strided_kernel, dim3((cols + 31) / 32, dbias ? 2 : 1), dim3(256), 0, s, part,
+                     kNormGrid * 4, cols, 2 * cols, dw, dbias);
+  return check_launch("mc_add_layernorm_bwd");
 }
 
 // VEC path when every row start is 16-B aligned and L is a whole number of vectors.

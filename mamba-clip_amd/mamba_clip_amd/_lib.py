@@ -89,6 +89,11 @@ SYMBOLS = {
     "mc_add_rmsnorm_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_fp, c_fp, c_fp, c_fp, c_vp, c_fp, c_fp, c_vp,
                                           ctypes.c_size_t, c_vp]),
     "mc_add_rmsnorm_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "mc_add_layernorm_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_vp, c_fp, c_fp, ctypes.c_float, c_vp, c_vp,
+                                            c_fp, c_fp, c_vp]),
+    "mc_add_layernorm_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_fp, c_fp, c_fp, c_vp, c_fp, c_fp,
+                                            c_vp, ctypes.c_size_t, c_vp]),
+    "mc_add_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "mc_causal_conv1d_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_i64, c_fp, c_fp, c_i32,
                                             c_vp, c_i64, c_i64, c_vp]),
     "mc_causal_conv1d_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_i64, c_fp, c_fp, c_i32,

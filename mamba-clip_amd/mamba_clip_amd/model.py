@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import add_rmsnorm, causal_conv1d, patch_im2col
+from .ops import add_layernorm, add_rmsnorm, causal_conv1d, patch_im2col
 from .selective_scan_interface import selective_scan_fn
 
 
@@ -180,6 +180,15 @@ class Attention(nn.Module):
 
 
 class ViTBlock(nn.Module):
+    """Pre-LN transformer block (timm Block parameters: norm1, attn, norm2, fc1/fc2 MLP).
+
+    forward(m, h) takes the previous block's branch output m and residual
+    stream h (x = h + m) and returns its own (m', h'): each residual add is
+    fused into the following LayerNorm (mc_add_layernorm), the way the Mamba
+    blocks fuse add + RMSNorm.  Same math as x = x + attn(norm1(x));
+    x = x + mlp(norm2(x)).
+    """
+
     def __init__(self, dim, heads, mlp_ratio=4.0):
         super().__init__()
         self.norm1 = nn.LayerNorm(dim, eps=1e-6)
@@ -188,9 +197,11 @@ class ViTBlock(nn.Module):
         self.fc1 = nn.Linear(dim, int(dim * mlp_ratio))
         self.fc2 = nn.Linear(int(dim * mlp_ratio), dim)
 
-    def forward(self, x):
-        x = x + self.attn(self.norm1(x))
-        return x + self.fc2(F.gelu(self.fc1(self.norm2(x))))
+    def forward(self, m, h=None):
+        y, h = add_layernorm(m, h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        a = self.attn(y)
+        y, h = add_layernorm(a, h, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        return self.fc2(F.gelu(self.fc1(y))), h
 
 
 class VisionTransformer(nn.Module):
@@ -215,10 +226,12 @@ class VisionTransformer(nn.Module):
     def forward(self, x):
         x = self.patch_embed(x)
         cls = self.cls_token.to(x.dtype).expand(x.shape[0], -1, -1)
-        x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
+        m, h = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype), None
         for blk in self.blocks:
-            x = blk(x)
-        return self.head(self.norm(x)[:, 0])
+            m, h = blk(m, h)
+        # final norm on the pooled (cls) rows only: same values as norm(x)[:, 0]
+        y, _ = add_layernorm(m[:, 0], h[:, 0], self.norm.weight, self.norm.bias, self.norm.eps)
+        return self.head(y)
 
     def lock(self, unlocked_groups=0, freeze_bn_stats=False):
         for p in self.parameters():
@@ -244,10 +257,10 @@ class BertTextEncoder(nn.Module):
         self.transformer = self.blocks
 
     def forward(self, tokens):
-        x = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]])
+        m, h = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]]), None
         for blk in self.blocks:
-            x = blk(x)
-        return self.proj(x[:, 0])
+            m, h = blk(m, h)
+        return self.proj(m[:, 0] + h[:, 0])
 
 
 # ============================================================================ CLIP wrapper (model.py:998-1112)

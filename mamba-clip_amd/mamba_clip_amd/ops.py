@@ -161,6 +161,92 @@ def add_rmsnorm(x, residual, weight, eps=1e-5):
     return AddRMSNormFn.apply(x, residual, weight, eps)
 
 
+class AddLayerNormFn(torch.autograd.Function):
+    """(y, h) = (LayerNorm(x + res) * w + b, x + res); h in the activation dtype (pre-LN residual stream)."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, eps):
+        lib = _lib.load()
+        x = x.contiguous()
+        res = res.to(x.dtype).contiguous()
+        cols = x.shape[-1]
+        rows = x.numel() // cols
+        y = torch.empty_like(x)
+        h = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        w = weight.float().contiguous()
+        b = bias.float().contiguous() if bias is not None else None
+        _lib.check(lib.mc_add_layernorm_fwd(rows, cols, _lib.dtype_code(x.dtype), x.data_ptr(), res.data_ptr(),
+                                            w.data_ptr(), _lib.ptr(b), float(eps), y.data_ptr(), h.data_ptr(),
+                                            mean.data_ptr(), rstd.data_ptr(), _lib.stream_handle(x.device)),
+                   "mc_add_layernorm_fwd")
+        ctx.save_for_backward(h, w, mean, rstd)
+        ctx.meta = (weight.dtype, bias.dtype if bias is not None else None)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _layernorm_bwd(h, w, mean, rstd, dy, dh, ctx.meta[1] is not None)
+        wdt, bdt = ctx.meta
+        return dx, dx, dw.to(wdt), (db.to(bdt) if db is not None else None), None
+
+
+class LayerNormFn(torch.autograd.Function):
+    """y = LayerNorm(x) * w + b with the activation dtype in and out (fp32 statistics)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        lib = _lib.load()
+        x = x.contiguous()
+        cols = x.shape[-1]
+        rows = x.numel() // cols
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        w = weight.float().contiguous()
+        b = bias.float().contiguous() if bias is not None else None
+        _lib.check(lib.mc_add_layernorm_fwd(rows, cols, _lib.dtype_code(x.dtype), x.data_ptr(), None, w.data_ptr(),
+                                            _lib.ptr(b), float(eps), y.data_ptr(), None, mean.data_ptr(),
+                                            rstd.data_ptr(), _lib.stream_handle(x.device)), "mc_add_layernorm_fwd")
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.meta = (weight.dtype, bias.dtype if bias is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _layernorm_bwd(x, w, mean, rstd, dy, None, ctx.meta[1] is not None)
+        wdt, bdt = ctx.meta
+        return dx, dw.to(wdt), (db.to(bdt) if db is not None else None), None
+
+
+def _layernorm_bwd(h, w, mean, rstd, dy, dh, has_bias):
+    lib = _lib.load()
+    cols = h.shape[-1]
+    rows = h.numel() // cols
+    dy = (dy if dy is not None else torch.zeros_like(h)).to(h.dtype).contiguous()
+    dh = dh.to(h.dtype).contiguous() if dh is not None else None
+    dx = torch.empty_like(h)
+    dw = torch.empty(cols, device=h.device, dtype=torch.float32)
+    db = torch.empty(cols, device=h.device, dtype=torch.float32) if has_bias else None
+    ws_b = lib.mc_add_layernorm_bwd_workspace_bytes(rows, cols)
+    ws = _ws(ws_b, h.device)
+    _lib.check(lib.mc_add_layernorm_bwd(rows, cols, _lib.dtype_code(h.dtype), dy.data_ptr(), _lib.ptr(dh),
+                                        h.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                        dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), ws_b,
+                                        _lib.stream_handle(h.device)), "mc_add_layernorm_bwd")
+    return dx, dw, db
+
+
+def add_layernorm(x, residual, weight, bias, eps=1e-6):
+    """Pre-LN block entry: returns (LN(x + residual), x + residual); residual None -> (LN(x), x)."""
+    if residual is None:
+        return LayerNormFn.apply(x, weight, bias, eps), x
+    return AddLayerNormFn.apply(x, residual, weight, bias, eps)
+
+
 class CausalConv1dFn(torch.autograd.Function):
     """Depthwise causal conv1d (+SiLU) over (batch, dim, seqlen); output contiguous."""
 

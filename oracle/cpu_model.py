@@ -1,7 +1,7 @@
 """CPU restatement of the stage-1 training step (TEST / BASELINE INFRASTRUCTURE ONLY).
 
 Used by bench.py's `cpu_baseline` leg and by tests: the SAME module classes
-as the product (mamba_clip_amd.model), with their four HIP entry points
+as the product (mamba_clip_amd.model), with their five HIP entry points
 swapped for the fp32 CPU restatements of this directory while the context is
 active, and the loss computed by oracle/loss_ref.clip_loss (loss.py:89-147).
 This is the "reference's CPU path" of SURVEY.md 8(d): fp32 PyTorch-CPU eager,
@@ -30,13 +30,19 @@ def _causal_conv1d_f32(x, w, b=None, silu=True):
     return F.silu(y) if silu else y
 
 
+def _add_layernorm_f32(x, res, w, b, eps=1e-6):
+    h = x if res is None else (x + res.to(x.dtype))
+    y = F.layer_norm(h.float(), (h.shape[-1],), w.float(), b.float() if b is not None else None, eps)
+    return y.to(x.dtype), h
+
+
 def _im2col(img, P):
     B, C, H, W = img.shape
     return F.unfold(img, P, stride=P).transpose(1, 2).reshape(B * (H // P) * (W // P), C * P * P)
 
 
 _OPS = {"selective_scan_fn": selective_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
-        "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col}
+        "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col, "add_layernorm": _add_layernorm_f32}
 
 
 @contextmanager

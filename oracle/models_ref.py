@@ -1,7 +1,7 @@
 """fp32 torch-CPU restatements of the encoder pieces (TEST INFRASTRUCTURE ONLY).
 
 Functional versions of the build's modules, fed the SAME parameters, used to
-check the HIP-backed modules: RMSNorm, depthwise causal conv1d, the Mamba
+check the HIP-backed modules: RMSNorm, residual-add + LayerNorm (timm pre-LN Block), depthwise causal conv1d, the Mamba
 mixer (conv -> x_proj/dt_proj -> selective scan -> gate -> out_proj; the
 reference's analogue is SS2D.forward, model.py:630-647, with the 1-D Mamba
 layout of mamba_ssm's Mamba), patch im2col (Conv2d k = s = P, model.py:189-191).
@@ -17,6 +17,17 @@ from .scan_ref import selective_scan_ref
 def rmsnorm_ref(x, res, w, eps=1e-5):
     h = x.double() + (res.double() if res is not None else 0)
     y = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * w.double()
+    return y, h
+
+
+def add_layernorm_ref(x, res, w, b, eps=1e-6, h_dtype=None):
+    """(LayerNorm(x + res), x + res) in fp64; h rounded to h_dtype first (the activation-dtype residual add)."""
+    h = x.double() + (res.double() if res is not None else 0)
+    if h_dtype is not None:
+        h = h.to(h_dtype).double()
+    mu = h.mean(-1, keepdim=True)
+    var = (h - mu).pow(2).mean(-1, keepdim=True)
+    y = (h - mu) * torch.rsqrt(var + eps) * w.double() + (b.double() if b is not None else 0)
     return y, h
 
 

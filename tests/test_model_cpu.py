@@ -1,4 +1,4 @@
-"""CPU checks of the module API (construction, shapes, parameter counts); no kernels run."""
+"""CPU checks of the module API (construction, shapes, parameter counts) and of the module wiring via the CPU restatement ops; no HIP kernels run."""
 import torch
 
 from mamba_clip_amd.model import MODEL_CONFIGS, ClipClassifier, build_clip, init_model
@@ -28,3 +28,28 @@ def test_classifier_head_shapes():
     assert head.fc[0].in_features == 64 and head.fc[0].out_features == 32
     assert all(not p.requires_grad for p in head.clip_model.parameters())
     assert ClipClassifier(clip, num_classes=3, use_inner_prod=True, feature_dim=32).fc[0].out_features == 32
+
+
+def test_fused_vit_blocks_equal_unfused_math_cpu():
+    """The (m, h) fused-residual ViT (CPU restatement ops) equals the textbook pre-LN recurrence."""
+    import torch.nn.functional as F
+    from mamba_clip_amd.model import VisionTransformer
+    from oracle.cpu_model import oracle_ops
+    torch.manual_seed(0)
+    vit = VisionTransformer(img_size=32, patch=8, width=64, layers=2, heads=4, output_dim=16)
+    img = torch.randn(3, 3, 32, 32)
+    with oracle_ops(), torch.no_grad():
+        out = vit(img)
+        x = vit.patch_embed.proj(img).flatten(2).transpose(1, 2)
+        x = torch.cat([vit.cls_token.expand(3, -1, -1), x], 1) + vit.pos_embed
+        for blk in vit.blocks:
+            x = x + blk.attn(blk.norm1(x))
+            x = x + blk.fc2(F.gelu(blk.fc1(blk.norm2(x))))
+        ref = vit.head(vit.norm(x)[:, 0])
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_cpu_restatement_train_step_runs():
+    from oracle.cpu_model import cpu_train_pairs_per_sec
+    pps, secs = cpu_train_pairs_per_sec("tiny-mamba-clip", batch=4, steps=1, warmup=1)
+    assert pps > 0 and secs > 0

@@ -2,6 +2,7 @@
 and the reference SS2D golden vectors."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 from conftest import load_golden
 from oracle import models_ref as R
@@ -36,6 +37,64 @@ def test_add_rmsnorm_fwd_bwd():
             torch.testing.assert_close(xd.grad.float().cpu(), xr.grad.float(), rtol=tol, atol=tol * 4)
             torch.testing.assert_close(rd.grad.cpu(), rr.grad.float(), rtol=1e-4, atol=1e-4)
             torch.testing.assert_close(wd.grad.cpu(), wr.grad.float(), rtol=1e-3, atol=1e-3 * rows ** 0.5)
+
+
+def test_add_layernorm_fwd_bwd():
+    from mamba_clip_amd.ops import add_layernorm
+    g = torch.Generator().manual_seed(5)
+    for dt in (torch.float32, torch.bfloat16):
+        for rows, cols, with_res, with_bias in [(9, 768, True, True), (197, 768, False, True), (5, 64, True, False)]:
+            x = torch.randn(rows, cols, generator=g).to(dt)
+            res = torch.randn(rows, cols, generator=g).to(dt) if with_res else None
+            w = 1 + 0.1 * torch.randn(cols, generator=g)
+            b = 0.1 * torch.randn(cols, generator=g) if with_bias else None
+            dy = torch.randn(rows, cols, generator=g).to(dt)
+            dh = torch.randn(rows, cols, generator=g).to(dt)
+            xd = x.to(DEV).requires_grad_(True)
+            rd = res.to(DEV).requires_grad_(True) if with_res else None
+            wd = w.to(DEV).requires_grad_(True)
+            bd = b.to(DEV).requires_grad_(True) if with_bias else None
+            y, h = add_layernorm(xd, rd, wd, bd)
+            loss = (y.float() * dy.to(DEV).float()).sum()
+            if with_res:
+                loss = loss + (h.float() * dh.to(DEV).float()).sum()
+            loss.backward()
+            xr = x.double().requires_grad_(True)
+            rr = res.double().requires_grad_(True) if with_res else None
+            wr = w.double().requires_grad_(True)
+            br = b.double().requires_grad_(True) if with_bias else None
+            yr, hr = R.add_layernorm_ref(xr, rr, wr, br)
+            lr = (yr * dy.double()).sum()
+            if with_res:
+                lr = lr + (hr * dh.double()).sum()
+            lr.backward()
+            tol = 1e-5 if dt == torch.float32 else 2e-2
+            torch.testing.assert_close(y.float().cpu(), yr.float(), rtol=tol, atol=tol)
+            torch.testing.assert_close(h.float().cpu(), hr.to(dt).float(), rtol=tol, atol=tol)
+            torch.testing.assert_close(xd.grad.float().cpu(), xr.grad.float(), rtol=tol, atol=tol * 4)
+            if with_res:
+                torch.testing.assert_close(rd.grad.float().cpu(), rr.grad.float(), rtol=tol, atol=tol * 4)
+            gtol = 1e-3 if dt == torch.float32 else 3e-2
+            torch.testing.assert_close(wd.grad.cpu(), wr.grad.float(), rtol=gtol, atol=gtol * rows ** 0.5)
+            if with_bias:
+                torch.testing.assert_close(bd.grad.cpu(), br.grad.float(), rtol=gtol, atol=gtol * rows ** 0.5)
+
+
+def test_vit_block_matches_unfused_math():
+    """Fused (m, h) ViT blocks == x = x + attn(norm1(x)); x = x + mlp(norm2(x)) in fp32."""
+    from mamba_clip_amd.model import VisionTransformer
+    torch.manual_seed(0)
+    vit = VisionTransformer(img_size=32, patch=8, width=64, layers=2, heads=4, output_dim=16).to(DEV)
+    img = torch.randn(3, 3, 32, 32, device=DEV)
+    out = vit(img)
+    with torch.no_grad():
+        x = vit.patch_embed.proj(img).flatten(2).transpose(1, 2)
+        x = torch.cat([vit.cls_token.expand(3, -1, -1), x], 1) + vit.pos_embed
+        for blk in vit.blocks:
+            x = x + blk.attn(blk.norm1(x))
+            x = x + blk.fc2(F.gelu(blk.fc1(blk.norm2(x))))
+        ref = vit.head(vit.norm(x)[:, 0])
+    torch.testing.assert_close(out.detach(), ref, rtol=1e-4, atol=1e-5)
 
 
 def test_causal_conv1d_fwd_bwd():
