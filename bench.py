@@ -136,6 +136,7 @@ def main():
     from mamba_clip_amd.loss import ClipLoss
     from mamba_clip_amd.model import build_clip
     from mamba_clip_amd.train import create_optimizer, train_step, wrap_ddp
+    from mamba_clip_amd.tuning import load_gemm_tuning
     from mamba_clip_amd.utils import init_device
 
     _lib.load()                                   # fail loudly if the HIP library is missing
@@ -143,6 +144,7 @@ def main():
                             grad_clip_norm=None, dist_backend="nccl", ddp_static_graph=True, accum_freq=1)
     device = init_device(targs)
     rank, world = targs.rank, targs.world_size
+    gemm_tuned = load_gemm_tuning()               # committed per-shape hipBLASLt/rocBLAS selection
     targs.lr *= world                             # pipeline.py:532
 
     torch.manual_seed(0)
@@ -191,7 +193,8 @@ def main():
                                "(fwd+bwd+AdamW), amp_bf16",
                    "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                    "seq_len": int(inner.text.context_length), "image_size": 224,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "library_gemm_selection": "tunableop-file" if gemm_tuned else "default-heuristic"},
         "mfma_estimate": {"flop_per_pair": C2_FLOP_PER_PAIR,
                           "achieved_tflops_per_gpu": round(value / world * C2_FLOP_PER_PAIR / 1e12, 1),
                           "peak": MFMA_BF16_DENSE_TFLOPS,

@@ -12,12 +12,29 @@ namespace mc {
 namespace ops {
 
 // ------------------------------------------------------------------ RMSNorm
-// One wave per row; the row lives in registers between the two passes
-// (cols <= kMaxCols).  Grid-stride over rows so the backward's per-wave dw
-// partials stay few (one slab row per wave).
+// One wave per row, the row in registers between the two passes; NV = 16-B
+// vectors per lane per row (cols <= 64 * NV * V).  The weight vectors a lane
+// touches are loaded once per wave (hoisted out of the row loop).  Grid-stride
+// over rows so the backward's per-wave dw partials stay few (one slab row per
+// wave).
 constexpr int kMaxVec = 8;  // 16-B vectors per lane per row: cols <= 4096 (16-bit) / 2048 (fp32)
 
-template <typename T>
+template <int V>
+__device__ __forceinline__ void ld_f32v(const float* __restrict__ p, float (&v)[V]) {
+#pragma unroll
+  for (int e4 = 0; e4 < V; e4 += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p + e4);
+    v[e4] = q.x; v[e4 + 1] = q.y; v[e4 + 2] = q.z; v[e4 + 3] = q.w;
+  }
+}
+template <int V>
+__device__ __forceinline__ void st_f32v(float* __restrict__ p, const float (&v)[V]) {
+#pragma unroll
+  for (int e4 = 0; e4 < V; e4 += 4)
+    *reinterpret_cast<float4*>(p + e4) = make_float4(v[e4], v[e4 + 1], v[e4 + 2], v[e4 + 3]);
+}
+
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols, const T* __restrict__ x,
                                                               const float* __restrict__ res_in,
                                                               const float* __restrict__ w, float eps,
@@ -28,23 +45,28 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int nvec = cols / V;
+  float wr[NV][V];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = lane + 64 * i;
+    if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
+  }
   for (int row = wave; row < rows; row += nwaves) {
-    float h[kMaxVec][V];
+    float h[NV][V];
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
-        const uint4 q = ld16(x + (int64_t)row * cols + v * V);
+        const int64_t off = (int64_t)row * cols + v * V;
+        const uint4 q = ld16(x + off);
 #pragma unroll
         for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(q, e);
         if (res_in) {
-          const float* r = res_in + (int64_t)row * cols + v * V;
+          float r[V];
+          ld_f32v<V>(res_in + off, r);
 #pragma unroll
-          for (int e4 = 0; e4 < V; e4 += 4) {
-            const float4 rq = *reinterpret_cast<const float4*>(r + e4);
-            h[i][e4] += rq.x; h[i][e4 + 1] += rq.y; h[i][e4 + 2] += rq.z; h[i][e4 + 3] += rq.w;
-          }
+          for (int e = 0; e < V; ++e) h[i][e] += r[e];
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) ss = fmaf(h[i][e], h[i][e], ss);
@@ -55,25 +77,21 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
     const float rs = rsqrtf(ss / cols + eps);
     if (lane == 0) rstd[row] = rs;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
         float o[V];
 #pragma unroll
-        for (int e = 0; e < V; ++e) o[e] = h[i][e] * rs * w[v * V + e];
-        st16(y + (int64_t)row * cols + v * V, pack_f<T>(o));
-        if (res_out) {
-          float* r = res_out + (int64_t)row * cols + v * V;
-#pragma unroll
-          for (int e4 = 0; e4 < V; e4 += 4)
-            *reinterpret_cast<float4*>(r + e4) = make_float4(h[i][e4], h[i][e4 + 1], h[i][e4 + 2], h[i][e4 + 3]);
-        }
+        for (int e = 0; e < V; ++e) o[e] = h[i][e] * rs * wr[i][e];
+        st16(y + off, pack_f<T>(o));
+        if (res_out) st_f32v<V>(res_out + off, h[i]);
       }
     }
   }
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                               const float* __restrict__ dres,
                                                               const float* __restrict__ hbuf,
@@ -86,26 +104,29 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int nvec = cols / V;
-  float dwacc[kMaxVec][V];
+  float wr[NV][V], dwacc[NV][V];
 #pragma unroll
-  for (int i = 0; i < kMaxVec; ++i)
+  for (int i = 0; i < NV; ++i) {
+    const int v = lane + 64 * i;
 #pragma unroll
     for (int e = 0; e < V; ++e) dwacc[i][e] = 0.f;
+    if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
+  }
   for (int row = wave; row < rows; row += nwaves) {
     const float rs = rstd[row];
-    float h[kMaxVec][V], g[kMaxVec][V];
+    float h[NV][V], g[NV][V];
     float dot = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
-        const uint4 q = ld16(dy + (int64_t)row * cols + v * V);
-        const float* hp = hbuf + (int64_t)row * cols + v * V;
+        const int64_t off = (int64_t)row * cols + v * V;
+        const uint4 q = ld16(dy + off);
+        ld_f32v<V>(hbuf + off, h[i]);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          h[i][e] = hp[e];
           const float d = elem_f<T>(q, e);
-          g[i][e] = d * w[v * V + e];
+          g[i][e] = d * wr[i][e];
           dot = fmaf(g[i][e], h[i][e], dot);
           dwacc[i][e] = fmaf(d, h[i][e] * rs, dwacc[i][e]);
         }
@@ -115,83 +136,76 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols
     for (int o = 32; o >= 1; o >>= 1) dot += __shfl_xor(dot, o);
     const float c = dot * rs * rs / cols;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
         float o[V];
+        float r[V];
+        if (dres) ld_f32v<V>(dres + off, r);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           o[e] = rs * (g[i][e] - h[i][e] * c);
-          if (dres) o[e] += dres[(int64_t)row * cols + v * V + e];
+          if (dres) o[e] += r[e];
         }
-        if (dx) st16(dx + (int64_t)row * cols + v * V, pack_f<T>(o));
-        if (dres_in) {
-          float* r = dres_in + (int64_t)row * cols + v * V;
-#pragma unroll
-          for (int e4 = 0; e4 < V; e4 += 4)
-            *reinterpret_cast<float4*>(r + e4) = make_float4(o[e4], o[e4 + 1], o[e4 + 2], o[e4 + 3]);
-        }
+        if (dx) st16(dx + off, pack_f<T>(o));
+        if (dres_in) st_f32v<V>(dres_in + off, o);
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < kMaxVec; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int v = lane + 64 * i;
-    if (v < nvec)
-#pragma unroll
-      for (int e = 0; e < V; ++e) dw_part[(int64_t)wave * cols + v * V + e] = dwacc[i][e];
+    if (v < nvec) st_f32v<V>(dw_part + (int64_t)wave * cols + v * V, dwacc[i]);
   }
 }
 
-// out[c] = sum_r in[r][c]: 32 columns x 8 row lanes per block, fixed order
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ in, int nrows, int cols,
-                                                     float* __restrict__ out) {
-  __shared__ float part[8][33];
-  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cx;
+// Deterministic column sums of a row-major partial slab in two passes:
+//   pass 1: grid (ceil(cols/256), kColSlices); thread = one column over a
+//           fixed row slice (coalesced across the block) -> tmp[slice][c]
+//   pass 2: thread = one column, sums the kColSlices partials in order.
+// Columns [0, split) land in out0, [split, cols) in out1 (out1 may be null).
+constexpr int kColSlices = 32;
+
+__global__ __launch_bounds__(256) void colsum_pass1_kernel(const float* __restrict__ in, int nrows, int cols,
+                                                           float* __restrict__ tmp) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int per = (nrows + kColSlices - 1) / kColSlices;
+  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
   float s = 0.f;
-  if (c < cols)
-    for (int r = q; r < nrows; r += 8) s += in[(int64_t)r * cols + c];
-  part[q][cx] = s;
-  __syncthreads();
-  if (q == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][cx];
-    out[c] = t;
-  }
+  for (int r = r0; r < r1; ++r) s += in[(int64_t)r * cols + c];
+  tmp[(int64_t)blockIdx.y * cols + c] = s;
 }
 
-// out_y[c] = sum_r in[r * ld + y * cols + c] for y = blockIdx.y (0 -> out0, 1 -> out1), fixed order
-__global__ __launch_bounds__(256) void colsum_strided_kernel(const float* __restrict__ in, int nrows, int cols,
-                                                             int64_t ld, float* __restrict__ out0,
-                                                             float* __restrict__ out1) {
-  __shared__ float part[8][33];
-  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cx;
-  const float* base = in + (int64_t)blockIdx.y * cols;
+__global__ __launch_bounds__(256) void colsum_pass2_kernel(const float* __restrict__ tmp, int cols, int split,
+                                                           float* __restrict__ out0, float* __restrict__ out1) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
   float s = 0.f;
-  if (c < cols)
-    for (int r = q; r < nrows; r += 8) s += base[(int64_t)r * ld + c];
-  part[q][cx] = s;
-  __syncthreads();
-  if (q == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][cx];
-    (blockIdx.y == 0 ? out0 : out1)[c] = t;
-  }
+#pragma unroll 8
+  for (int k = 0; k < kColSlices; ++k) s += tmp[(int64_t)k * cols + c];
+  if (c < split) out0[c] = s;
+  else if (out1) out1[c - split] = s;
 }
 
-constexpr int kNormGrid = 256;  // blocks of 4 waves: 1024 waves -> 1024 dw partial rows
+static void colsum_two_pass(const float* in, int nrows, int cols, int split, float* out0, float* out1, float* tmp,
+                            hipStream_t s) {
+  const int gx = (cols + 255) / 256;
+  hipLaunchKernelGGL(colsum_pass1_kernel, dim3(gx, kColSlices), dim3(256), 0, s, in, nrows, cols, tmp);
+  hipLaunchKernelGGL(colsum_pass2_kernel, dim3(gx), dim3(256), 0, s, tmp, cols, split, out0, out1);
+}
+
+constexpr int kNormGrid = 512;  // blocks of 4 waves: 2048 waves -> 2048 dw partial rows
 
 // ------------------------------------------------------------------ residual-add + LayerNorm
 // ViT/BERT pre-LN blocks: h = x + res (stored in the activation dtype, the
 // same rounding as the autocast residual add), y = (h - mean) * rstd * w + b
 // in fp32 math, stored in the activation dtype.  One wave per row, the row in
-// registers; the backward recomputes xhat from h and emits per-wave dw/db
-// partials reduced by colsum_kernel (deterministic).
-template <typename T>
+// registers, weights hoisted per wave; the backward recomputes xhat from h
+// and emits per-wave dw/db partials reduced by colsum_two_pass
+// (deterministic).
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int cols, const T* __restrict__ x,
                                                                 const T* __restrict__ res,
                                                                 const float* __restrict__ w,
@@ -204,24 +218,32 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int nvec = cols / V;
+  float wr[NV][V], br[NV][V];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = lane + 64 * i;
+    if (v < nvec) {
+      ld_f32v<V>(w + v * V, wr[i]);
+      if (bias) ld_f32v<V>(bias + v * V, br[i]);
+      else
+#pragma unroll
+        for (int e = 0; e < V; ++e) br[i][e] = 0.f;
+    }
+  }
   for (int row = wave; row < rows; row += nwaves) {
-    float h[kMaxVec][V];
+    float h[NV][V];
     float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
         const int64_t off = (int64_t)row * cols + v * V;
         const uint4 q = ld16(x + off);
         if (res) {
           const uint4 r = ld16(res + off);
-          float hv[V];
 #pragma unroll
-          for (int e = 0; e < V; ++e) hv[e] = to_f(from_f<T>(elem_f<T>(q, e) + elem_f<T>(r, e)));
-          const uint4 hq = pack_f<T>(hv);
-          if (h_out) st16(h_out + off, hq);
-#pragma unroll
-          for (int e = 0; e < V; ++e) h[i][e] = hv[e];
+          for (int e = 0; e < V; ++e) h[i][e] = to_f(from_f<T>(elem_f<T>(q, e) + elem_f<T>(r, e)));
+          if (h_out) st16(h_out + off, pack_f<T>(h[i]));
         } else {
 #pragma unroll
           for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(q, e);
@@ -235,7 +257,7 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
     const float mu = sum / cols;
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec)
 #pragma unroll
@@ -246,13 +268,12 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
     const float rs = rsqrtf(ss / cols + eps);
     if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
         float o[V];
 #pragma unroll
-        for (int e = 0; e < V; ++e)
-          o[e] = fmaf((h[i][e] - mu) * rs, w[v * V + e], bias ? bias[v * V + e] : 0.f);
+        for (int e = 0; e < V; ++e) o[e] = fmaf((h[i][e] - mu) * rs, wr[i][e], br[i][e]);
         st16(y + (int64_t)row * cols + v * V, pack_f<T>(o));
       }
     }
@@ -261,7 +282,7 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
 
 // dh_total = dh + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // dx (= dres) = dh_total;  part rows: [wave][0..cols) dw, [wave][cols..2cols) db
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                                 const T* __restrict__ dh,
                                                                 const T* __restrict__ hbuf,
@@ -274,17 +295,20 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int nvec = cols / V;
-  float dwacc[kMaxVec][V], dbacc[kMaxVec][V];
+  float wr[NV][V], dwacc[NV][V], dbacc[NV][V];
 #pragma unroll
-  for (int i = 0; i < kMaxVec; ++i)
+  for (int i = 0; i < NV; ++i) {
+    const int v = lane + 64 * i;
 #pragma unroll
     for (int e = 0; e < V; ++e) { dwacc[i][e] = 0.f; dbacc[i][e] = 0.f; }
+    if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
+  }
   for (int row = wave; row < rows; row += nwaves) {
     const float mu = mean[row], rs = rstd[row];
-    float xh[kMaxVec][V], g[kMaxVec][V];
+    float xh[NV][V], g[NV][V];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
         const int64_t off = (int64_t)row * cols + v * V;
@@ -294,7 +318,7 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
         for (int e = 0; e < V; ++e) {
           const float d = elem_f<T>(q, e);
           xh[i][e] = (elem_f<T>(hq, e) - mu) * rs;
-          g[i][e] = d * w[v * V + e];
+          g[i][e] = d * wr[i][e];
           sg += g[i][e];
           sgx = fmaf(g[i][e], xh[i][e], sgx);
           dwacc[i][e] = fmaf(d, xh[i][e], dwacc[i][e]);
@@ -309,7 +333,7 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
     }
     const float mg = sg / cols, mgx = sgx / cols;
 #pragma unroll
-    for (int i = 0; i < kMaxVec; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
         const int64_t off = (int64_t)row * cols + v * V;
@@ -326,16 +350,27 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
     }
   }
 #pragma unroll
-  for (int i = 0; i < kMaxVec; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int v = lane + 64 * i;
-    if (v < nvec)
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        part[(int64_t)wave * 2 * cols + v * V + e] = dwacc[i][e];
-        part[(int64_t)wave * 2 * cols + cols + v * V + e] = dbacc[i][e];
-      }
+    if (v < nvec) {
+      st_f32v<V>(part + (int64_t)wave * 2 * cols + v * V, dwacc[i]);
+      st_f32v<V>(part + (int64_t)wave * 2 * cols + cols + v * V, dbacc[i]);
+    }
   }
 }
+
+// vectors per lane per row -> template instance
+static inline int norm_nv(int cols, int V) {
+  const int per = (cols / V + 63) / 64;
+  return per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
+}
+#define MC_DISPATCH_NV(nv, ...)                                   \
+  do {                                                            \
+    if ((nv) == 1) { constexpr int NV = 1; __VA_ARGS__; }         \
+    else if ((nv) == 2) { constexpr int NV = 2; __VA_ARGS__; }    \
+    else if ((nv) == 4) { constexpr int NV = 4; __VA_ARGS__; }    \
+    else { constexpr int NV = 8; __VA_ARGS__; }                   \
+  } while (0)
 
 // ------------------------------------------------------------------ causal conv1d
 // Vector tiles along the sequence: each work item owns VEC consecutive
@@ -524,11 +559,11 @@ __global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restr
   else if (dbias) dbias[d] = s;
 }
 
-// batch x chunk items per backward wave: ~8 items per lane
+// batch x chunk items per backward wave: ~4 items per lane
 static inline int conv1d_items_per_slice(int batch, int L, int vec) {
   const int nchunk = (L + vec - 1) / vec;
   const int total = batch * nchunk;
-  const int target = 64 * 8;
+  const int target = 64 * 4;            // 4 items per lane: enough waves to hide the load latency
   const int nslice = std::max(1, (total + target - 1) / target);
   return (total + nslice - 1) / nslice;
 }
@@ -579,14 +614,14 @@ extern "C" int mc_add_rmsnorm_fwd(int32_t rows, int32_t cols, int32_t dtype, con
   MC_CHECK(x && w && y && rstd && aligned16(x) && aligned16(y), MC_ERR_INVALID,
            "mc_add_rmsnorm_fwd: x, w, y, rstd required (x, y 16-B aligned)");
   const int grid = std::min((rows + 3) / 4, 4096);
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_rmsnorm_fwd_kernel<T>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                                          rows, cols, (const T*)x, res_in, w, eps, (T*)y, res_out, rstd));
+  MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_rmsnorm_fwd_kernel<T, NV>), dim3(grid),
+      dim3(256), 0, (hipStream_t)stream, rows, cols, (const T*)x, res_in, w, eps, (T*)y, res_out, rstd)));
   return check_launch("mc_add_rmsnorm_fwd");
 }
 
 extern "C" size_t mc_add_rmsnorm_bwd_workspace_bytes(int32_t rows, int32_t cols) {
   (void)rows;
-  return (size_t)kNormGrid * 4 * cols * sizeof(float);
+  return ((size_t)kNormGrid * 4 + kColSlices) * cols * sizeof(float);   // per-wave partials + column-sum slices
 }
 
 extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const float* dres,
@@ -601,9 +636,9 @@ extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, con
            "mc_add_rmsnorm_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   float* part = reinterpret_cast<float*>(workspace);
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_rmsnorm_bwd_kernel<T>), dim3(kNormGrid), dim3(256), 0, s, rows, cols,
-                                          (const T*)dy, dres, h, w, rstd, (T*)dx, dres_in, part));
-  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, kNormGrid * 4, cols, dw);
+  MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_rmsnorm_bwd_kernel<T, NV>),
+      dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, dres, h, w, rstd, (T*)dx, dres_in, part)));
+  colsum_two_pass(part, kNormGrid * 4, cols, cols, dw, nullptr, part + (size_t)kNormGrid * 4 * cols, s);
   return check_launch("mc_add_rmsnorm_bwd");
 }
 
@@ -619,15 +654,15 @@ extern "C" int mc_add_layernorm_fwd(int32_t rows, int32_t cols, int32_t dtype, c
                (!h_out || aligned16(h_out)),
            MC_ERR_INVALID, "mc_add_layernorm_fwd: x, w, y, mean, rstd required (16-B aligned rows)");
   const int grid = std::min((rows + 3) / 4, 4096);
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_layernorm_fwd_kernel<T>), dim3(grid), dim3(256), 0,
-                                          (hipStream_t)stream, rows, cols, (const T*)x, (const T*)res, w, bias, eps,
-                                          (T*)y, (T*)h_out, mean, rstd));
+  MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_fwd_kernel<T, NV>),
+      dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols, (const T*)x, (const T*)res, w, bias, eps, (T*)y,
+      (T*)h_out, mean, rstd)));
   return check_launch("mc_add_layernorm_fwd");
 }
 
 extern "C" size_t mc_add_layernorm_bwd_workspace_bytes(int32_t rows, int32_t cols) {
   (void)rows;
-  return (size_t)kNormGrid * 4 * 2 * cols * sizeof(float);
+  return ((size_t)kNormGrid * 4 + kColSlices) * 2 * cols * sizeof(float);   // per-wave dw|db partials + slices
 }
 
 extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const void* dh,
@@ -643,12 +678,11 @@ extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, c
            "mc_add_layernorm_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   float* part = reinterpret_cast<float*>(workspace);
-  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((add_layernorm_bwd_kernel<T>), dim3(kNormGrid), dim3(256), 0, s, rows,
-                                          cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
-                                          part));
+  MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_bwd_kernel<T, NV>),
+      dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
+      part)));
   // part is [wave][2 * cols]: dw in columns [0, cols), dbias in [cols, 2 cols)
-  hipLaunchKernelGGL(colsum_strided_kernel, dim3((cols + 31) / 32, dbias ? 2 : 1), dim3(256), 0, s, part,
-                     kNormGrid * 4, cols, 2 * cols, dw, dbias);
+  colsum_two_pass(part, kNormGrid * 4, 2 * cols, cols, dw, dbias, part + (size_t)kNormGrid * 4 * 2 * cols, s);
   return check_launch("mc_add_layernorm_bwd");
 }
 

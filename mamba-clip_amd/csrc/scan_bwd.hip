@@ -15,15 +15,24 @@
 //    walked in reverse; each tile restarts from the fp32 state the training
 //    forward saved at its start (chunk_states), so nothing is recomputed
 //    across tiles.
-//  * inside a tile the state index n is the outer (fully unrolled) loop: a
-//    forward sweep keeps x_t,n and a_t,n for the 16 positions in VGPRs, the
-//    reverse sweep consumes them; per-position accumulators (du, ddt, y) stay
-//    in VGPRs across n.
+//  * each lane reads / writes its own row's positions as 16-B vectors (no
+//    LDS staging of the rows).  LDS holds the B/C tile and the per-lane,
+//    per-state scalars (A, tile-start state, mid-tile state, adjoint carry;
+//    18 KB per wave at dstate 16) so the n-loop never waits on global memory.
+//  * the n-loop runs on 8-position sub-tiles (register budget); the state at
+//    the middle of a 16-position tile is recomputed from the saved tile-start
+//    state by a short forward pre-pass.
+//  * inside a tile the state index n is the outer loop: a forward sweep keeps
+//    x_t,n and a_t,n for the 16 positions in VGPRs, the reverse sweep consumes
+//    them; per-position accumulators stay in VGPRs across n:
+//      S_t = sum_n h B,  Q_t = sum_n h A a x_{t-1},  y_t = sum_n C x
+//    so du = dt S + D gy and ddt = Q + u S need no per-n work.
 //  * dB/dC (sums over the 64 channels of the wave) use an in-register
 //    transpose-reduce: permlane32_swap / permlane16_swap / DPP row_ror:8 /
-//    ds_swizzle / quad_perm halving stages turn 32 per-lane values into 32 wave sums in
-//    ~2 VALU per value, then land in a per-wave fp32 slab.  A small second
-//    kernel sums the slabs over waves / batches: deterministic, no atomics.
+//    ds_swizzle / quad_perm halving stages turn 16 per-lane values into 16
+//    wave sums in ~2 VALU per value, then land in a per-wave fp32 slab.  A
+//    small second kernel sums the slabs over waves / batches: deterministic,
+//    no atomics.
 #include "scan_common.h"
 
 namespace mc {
@@ -40,7 +49,7 @@ struct BwdArgs {
   const float* chunk_states;
   void* du; void* ddelta; void* dz;
   float* slab_bc;                    // [b*G+g][nblk][kN][2][seqlen]
-  float* slab_a;                     // [b][dim][kN]
+  float* slab_a;                     // [b][kN][dim] (dA partials, one owner per element)
   float* slab_d;                     // [b][dim]
   float* slab_bias;                  // [b][dim]
 };
@@ -59,59 +68,89 @@ __device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
   return __int_as_float(r);
 }
 
-// 32 per-lane values -> 32 sums over the wave's 64 lanes.  Afterwards lane l
-// holds the sum of value index l >> 1 (both lanes of a pair hold it).
-__device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lane) {
+// NV per-lane values -> NV sums over the wave's 64 lanes (NV in {8, 16, 32}).
+// Halving stages over lane bits 5, 4, 3, ... pair value j with j + NV/2^k;
+// the remaining low lane bits are summed in full.  Afterwards lane l holds
+// the sum of value index l / (64 / NV).
+template <int NV>
+__device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane) {
+  static_assert(NV == 8 || NV == 16 || NV == 32, "NV in {8, 16, 32}");
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {  // bit 5: lanes 0-31 keep [0,16), lanes 32-63 keep [16,32)
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 16]), false, false);
+  for (int j = 0; j < NV / 2; ++j) {   // lane bit 5
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + NV / 2]), false, false);
     v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {   // bit 4: even 16-lane rows keep [0,8), odd rows keep [8,16)
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 8]), false, false);
+  for (int j = 0; j < NV / 4; ++j) {   // lane bit 4
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + NV / 4]), false, false);
     v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
   const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {   // bit 3 via row_ror:8 (== xor 8 inside a row)
-    const float keep = b3 ? v[j + 4] : v[j], send = b3 ? v[j] : v[j + 4];
+  for (int j = 0; j < NV / 8; ++j) {   // lane bit 3 via row_ror:8 (== xor 8 inside a row)
+    const float keep = b3 ? v[j + NV / 8] : v[j], send = b3 ? v[j] : v[j + NV / 8];
     v[j] = keep + dpp_f(send, 0);
   }
+  if constexpr (NV >= 16) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {   // bit 2 via ds_swizzle xor 4
-    const float keep = b2 ? v[j + 2] : v[j], send = b2 ? v[j] : v[j + 2];
-    v[j] = keep + dpp_f(send, 1);
+    for (int j = 0; j < NV / 16; ++j) {   // lane bit 2 via ds_swizzle xor 4
+      const float keep = b2 ? v[j + NV / 16] : v[j], send = b2 ? v[j] : v[j + NV / 16];
+      v[j] = keep + dpp_f(send, 1);
+    }
+  } else {
+    v[0] += dpp_f(v[0], 1);
   }
-  {                               // bit 1 via quad_perm [2,3,0,1]
+  if constexpr (NV >= 32) {             // lane bit 1 via quad_perm [2,3,0,1]
     const float keep = b1 ? v[1] : v[0], send = b1 ? v[0] : v[1];
     v[0] = keep + dpp_f(send, 2);
+  } else {
+    v[0] += dpp_f(v[0], 2);
   }
-  return v[0] + dpp_f(v[0], 3);  // bit 0 via quad_perm [1,0,3,2]
+  return v[0] + dpp_f(v[0], 3);         // lane bit 0 via quad_perm [1,0,3,2]
 }
 
-// Raw row (staging) and processed row share one LDS region per lane.
+constexpr int kSub = kTB / 2;            // positions per sub-tile of the n-loop (8)
+
+// Own-row vector I/O: a lane reads / writes kSub consecutive positions of its
+// own (b, d) row as 16-B vectors (no LDS staging: a wave revisits its rows
+// tile after tile, so L2 sees whole lines).
 template <typename TI>
-struct BwdRow {
-  static constexpr int kRawArr = kTB * (int)sizeof(TI);  // bytes of one raw array segment
-  static constexpr int kRawBytes = 4 * kRawArr;          // u, delta, z, dout
-  static constexpr int kProcBytes = 4 * kTB * 4;         // 4 fp32 arrays of kTB
-  static constexpr int kBytes = kRawBytes > kProcBytes ? kRawBytes : kProcBytes;
-  static constexpr int kStride = kBytes + 16;
-};
+__device__ __forceinline__ void load_row_sub(const TI* __restrict__ p, int l0, int L, bool full,
+                                             uint4 (&q)[kSub / ElemTraits<TI>::kVec]) {
+  constexpr int VI = ElemTraits<TI>::kVec;
+#pragma unroll
+  for (int k = 0; k < kSub / VI; ++k) {
+    const int col0 = l0 + k * VI;
+    if (full) q[k] = ld16(p + col0);
+    else q[k] = ld16_masked(p + col0, max(0, min(VI, L - col0)));
+  }
+}
+
+template <typename TI>
+__device__ __forceinline__ void store_row_sub(TI* __restrict__ p, int l0, int L, bool full, const float (&v)[kSub]) {
+  constexpr int VI = ElemTraits<TI>::kVec;
+#pragma unroll
+  for (int k = 0; k < kSub / VI; ++k) {
+    float w[VI];
+#pragma unroll
+    for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
+    const int col0 = l0 + k * VI;
+    if (full) st16(p + col0, pack_f<TI>(w));
+    else st16_masked(p + col0, pack_f<TI>(w), max(0, min(VI, L - col0)));
+  }
+}
 
 template <typename TI, int kN, bool kAligned>
 __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
-  using RW = BwdRow<TI>;
   constexpr int VI = ElemTraits<TI>::kVec;
-  constexpr int kVPR = kTB / VI;        // 16-B vectors per raw row segment (2 for 16-bit, 4 for fp32)
+  constexpr int kVPS = kSub / VI;   // 16-B vectors per sub-tile of one row (1 for 16-bit, 2 for fp32)
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* rowbuf = smem;                                                  // [64][kStride]
-  float* bcT = reinterpret_cast<float*>(smem + kRows * RW::kStride);    // [2kN][kTB]: B rows then C rows
-  // per-lane, per-state scalars, [slot][n][lane] (lane-minor: conflict-free):
-  // slot 0 = A*log2e, 1 = tile start state, 2 = adjoint carry, 3 = dA accumulator
-  float* lst = bcT + 2 * kN * kTB;
+  extern __shared__ __attribute__((aligned(16))) float smem_f[];
+  float* bcT = smem_f;                   // [2kN][kTB]: B rows then C rows of this tile
+  float* carry = bcT + 2 * kN * kTB;     // [kN][kRows]: adjoint carried into the previous positions
+  float* xmid = carry + kN * kRows;      // [kN][kRows]: state after the tile's first sub-tile
+  float* x0s = xmid + kN * kRows;        // [kN][kRows]: saved state at the tile start
+  float* a2s = x0s + kN * kRows;         // [kN][kRows]: A * log2(e)
 
   const int lane = threadIdx.x;
   const int lin = xcd_remap(blockIdx.x, a.total_blocks);
@@ -126,54 +165,77 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   const bool softplus = a.softplus != 0;
   const int my_d = dbase + lane;
   const bool my_ok = lane < nrows;
-  const int my_dc = dbase + min(lane, nrows - 1);
+  const int my_dc = dbase + min(lane, nrows - 1);   // lanes past the group end mirror a valid row (never stored)
 
-  const TI* __restrict__ u = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs;
-  const TI* __restrict__ dl = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs;
-  const TI* __restrict__ zp = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs;
-  const TI* __restrict__ gop = reinterpret_cast<const TI*>(a.dout) + (int64_t)b * a.go_bs;
+  const TI* __restrict__ urow = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs + (int64_t)my_dc * a.u_ds;
+  const TI* __restrict__ drow = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs + (int64_t)my_dc * a.dt_ds;
+  const TI* __restrict__ zrow = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs + (int64_t)my_dc * a.z_ds;
+  const TI* __restrict__ grow = reinterpret_cast<const TI*>(a.dout) + (int64_t)b * a.go_bs + (int64_t)my_dc * a.go_ds;
+  TI* __restrict__ durow = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)my_dc * a.du_ds;
+  TI* __restrict__ ddrow = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)my_dc * a.ddt_ds;
+  TI* __restrict__ dzrow = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)my_dc * a.dz_ds;
+  const float* __restrict__ Arow = a.A + (int64_t)my_dc * a.dstate;
+  const float* __restrict__ csrow = a.chunk_states + ((int64_t)b * a.dim + my_dc) * a.n_states * a.dstate;
 
+  // per-lane, per-state scalars live in LDS ([n][lane]: conflict-free) so the
+  // n-loop never waits on global memory
 #pragma unroll
   for (int n = 0; n < kN; ++n) {
-    lst[(0 * kN + n) * kRows + lane] = (n < a.dstate) ? a.A[(int64_t)my_dc * a.dstate + n] * kLog2e : 0.f;
-    lst[(2 * kN + n) * kRows + lane] = 0.f;
-    lst[(3 * kN + n) * kRows + lane] = 0.f;
+    carry[n * kRows + lane] = 0.f;
+    a2s[n * kRows + lane] = n < a.dstate ? Arow[n] * kLog2e : 0.f;
   }
+  // dA_n accumulators: a register ring rotated once per n step (the n-loop is
+  // not unrolled), so dAr[0] always belongs to the current n
+  float dAr[kN];
+#pragma unroll
+  for (int n = 0; n < kN; ++n) dAr[n] = 0.f;
   const float Dv = a.D ? a.D[my_dc] : 0.f;
   const float biasv = a.delta_bias ? a.delta_bias[my_dc] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
 
+  // raw vectors of one sub-tile -> per-position scalars
+  auto prep = [&](const uint4 (&rd)[kVPS], const uint4 (&ru)[kVPS], const uint4 (&rz)[kVPS],
+                  const uint4 (&rg)[kVPS], int p0, int t, float& dtv, float& sgv, float& uv, float& gyv, float& gzv) {
+    uv = elem_f<TI>(ru[t / VI], t % VI);
+    const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
+    const float go = elem_f<TI>(rg[t / VI], t % VI);
+    const bool live = p0 + t < L_;
+    const float d = softplus ? softplus_f(r) : r;
+    // d softplus/dr = sigmoid(r) (torch: gradient 1 above the threshold 20)
+    sgv = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
+    dtv = live ? d : 0.f;
+    if (hasZ) {
+      const float zv = elem_f<TI>(rz[t / VI], t % VI);
+      const float sgz = sigmoid_f(zv);
+      gyv = go * zv * sgz;                              // dout * silu(z)
+      gzv = go * sgz * (1.f + zv * (1.f - sgz));        // dout * silu'(z)
+    } else {
+      gyv = go;
+      gzv = 0.f;
+    }
+  };
+  auto load_raw = [&](int p0, bool full, uint4 (&ru)[kVPS], uint4 (&rd)[kVPS], uint4 (&rz)[kVPS],
+                      uint4 (&rg)[kVPS]) {
+    load_row_sub<TI>(urow, p0, L_, full, ru);
+    load_row_sub<TI>(drow, p0, L_, full, rd);
+    if (hasZ) {
+      load_row_sub<TI>(zrow, p0, L_, full, rz);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kVPS; ++k) rz[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    load_row_sub<TI>(grow, p0, L_, full, rg);
+  };
+
   const int ntiles = (L_ + kTB - 1) / kTB;
   for (int ti = ntiles - 1; ti >= 0; --ti) {
     const int l0 = ti * kTB;
-    const bool full = kAligned && (l0 + kTB <= L_);
-    __syncthreads();  // previous tile's output pass is done with the rows
-
-    // ---- stage raw u / delta / z / dout (coalesced along the sequence)
+    const bool has_hi = l0 + kSub < L_;            // second sub-tile has live positions
+    __syncthreads();  // previous tile is done with bcT / xmid / x0s
+    // saved tile-start state -> LDS (zero for the first tile)
 #pragma unroll
-    for (int k = 0; k < kVPR; ++k) {
-      const int j = lane + k * kRows;
-      const int r = j / kVPR, c = j % kVPR;
-      const int rr = min(r, nrows - 1);
-      const int col0 = l0 + c * VI;
-      const int nv = max(0, min(VI, L_ - col0));
-      const int64_t ro = dbase + rr;
-      const TI* s0 = u + ro * a.u_ds + col0;
-      const TI* s1 = dl + ro * a.dt_ds + col0;
-      const TI* s2 = zp + ro * a.z_ds + col0;
-      const TI* s3 = gop + ro * a.go_ds + col0;
-      const uint4 q0 = full ? ld16(s0) : ld16_masked(s0, nv);
-      const uint4 q1 = full ? ld16(s1) : ld16_masked(s1, nv);
-      const uint4 q2 = hasZ ? (full ? ld16(s2) : ld16_masked(s2, nv)) : make_uint4(0u, 0u, 0u, 0u);
-      const uint4 q3 = full ? ld16(s3) : ld16_masked(s3, nv);
-      char* row = rowbuf + r * RW::kStride + c * 16;
-      st16(row, q0);
-      st16(row + RW::kRawArr, q1);
-      st16(row + 2 * RW::kRawArr, q2);
-      st16(row + 3 * RW::kRawArr, q3);
-    }
-    // ---- B/C tile, transposed to [2kN][kTB] (per-n rows of positions)
-    {
+    for (int n = 0; n < kN; ++n) x0s[n * kRows + lane] = (ti > 0 && n < a.dstate) ? csrow[(ti - 1) * a.dstate + n] : 0.f;
+    {   // B/C tile, transposed to [2kN][kTB] (per-n rows of positions)
       const float* src = a.bct + ((int64_t)bg * L_ + l0) * (2 * kN);
       const int nval = min(kTB, L_ - l0) * (2 * kN);
       for (int v = lane; v < kTB * 2 * kN; v += kRows) {
@@ -183,180 +245,142 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
     }
     __syncthreads();
 
-    // ---- per-position scalars of my channel
-    float dt[kTB], uu[kTB], gy[kTB];
-    float* prow = reinterpret_cast<float*>(rowbuf + lane * RW::kStride);  // processed: gz @ [2kTB], sg @ [3kTB]
-    {
-      const char* row = rowbuf + lane * RW::kStride;
-      uint4 ru[kVPR], rd[kVPR], rz[kVPR], rg[kVPR];
+    // ---- state after the first sub-tile (restart point of the second), from the saved tile-start state
+    if (has_hi) {
+      float dt[kSub], dtu[kSub];
+      {
+        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
+        load_raw(l0, kAligned, ru, rd, rz, rg);   // l0 + kSub < L: the first sub-tile is full
 #pragma unroll
-      for (int k = 0; k < kVPR; ++k) {
-        ru[k] = ld16(row + k * 16);
-        rd[k] = ld16(row + RW::kRawArr + k * 16);
-        rz[k] = ld16(row + 2 * RW::kRawArr + k * 16);
-        rg[k] = ld16(row + 3 * RW::kRawArr + k * 16);
-      }
-      float gz[kTB], sg[kTB];
-#pragma unroll
-      for (int t = 0; t < kTB; ++t) {
-        const float uv = elem_f<TI>(ru[t / VI], t % VI);
-        const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
-        const float go = elem_f<TI>(rg[t / VI], t % VI);
-        const bool live = l0 + t < L_;
-        float d = softplus ? softplus_f(r) : r;
-        // d softplus/dr = sigmoid(r) (torch: grad 1 above the threshold 20)
-        float s = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
-        d = live ? d : 0.f;
-        dt[t] = d;
-        sg[t] = s;
-        uu[t] = uv;
-        if (hasZ) {
-          const float zv = elem_f<TI>(rz[t / VI], t % VI);
-          const float sgz = sigmoid_f(zv);
-          gy[t] = go * zv * sgz;                                   // dout * silu(z)
-          gz[t] = go * sgz * (1.f + zv * (1.f - sgz));             // dout * silu'(z)
-        } else {
-          gy[t] = go;
-          gz[t] = 0.f;
+        for (int t = 0; t < kSub; ++t) {
+          float sgv, uv, gyv, gzv;
+          prep(rd, ru, rz, rg, l0, t, dt[t], sgv, uv, gyv, gzv);
+          dtu[t] = dt[t] * uv;
         }
       }
-      // all lanes' raw reads precede these writes (one wave, program order)
+#pragma unroll 1
+      for (int n = 0; n < kN; ++n) {
+        const float A2n = a2s[n * kRows + lane];
+        float x = x0s[n * kRows + lane];
+        const float* Bt = bcT + n * kTB;
 #pragma unroll
-      for (int t4 = 0; t4 < kTB; t4 += 4) {
-        *reinterpret_cast<float4*>(prow + 2 * kTB + t4) = make_float4(gz[t4], gz[t4 + 1], gz[t4 + 2], gz[t4 + 3]);
-        *reinterpret_cast<float4*>(prow + 3 * kTB + t4) = make_float4(sg[t4], sg[t4 + 1], sg[t4 + 2], sg[t4 + 3]);
+        for (int t = 0; t < kSub; ++t) x = fmaf(fast_exp2(dt[t] * A2n), x, dtu[t] * Bt[t]);
+        xmid[n * kRows + lane] = x;
       }
     }
 
-    // ---- tile start state (saved by the forward), zero for the first tile
-    {
-      const float* cs = a.chunk_states + (((int64_t)b * a.dim + my_dc) * a.n_states + max(ti - 1, 0)) * a.dstate;
+    // ---- the two sub-tiles, last first
+#pragma unroll 1
+    for (int sub = has_hi ? 1 : 0; sub >= 0; --sub) {
+      const int p0 = l0 + sub * kSub;
+      const bool full = kAligned && (p0 + kSub <= L_);
+      float dt[kSub], dtu[kSub], gy[kSub];
+      {
+        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
+        load_raw(p0, full, ru, rd, rz, rg);
 #pragma unroll
-      for (int n = 0; n < kN; ++n) lst[(1 * kN + n) * kRows + lane] = (ti > 0 && n < a.dstate) ? cs[n] : 0.f;
-    }
-
-    float ys[kTB], du[kTB], ddt[kTB];
+        for (int t = 0; t < kSub; ++t) {
+          float sgv, uv, gzv;
+          prep(rd, ru, rz, rg, p0, t, dt[t], sgv, uv, gy[t], gzv);
+          dtu[t] = dt[t] * uv;
+        }
+      }
+      // S_t = sum_n h B ;  Q_t = sum_n h A a x_{t-1} ;  ys_t = sum_n C x
+      float ys[kSub], S[kSub], Q[kSub];
 #pragma unroll
-    for (int t = 0; t < kTB; ++t) { ys[t] = 0.f; du[t] = 0.f; ddt[t] = 0.f; }
+      for (int t = 0; t < kSub; ++t) { ys[t] = 0.f; S[t] = 0.f; Q[t] = 0.f; }
 
 #pragma unroll 1
-    for (int n = 0; n < kN; ++n) {
-      const float A2n = lst[(0 * kN + n) * kRows + lane];
-      const float x0n = lst[(1 * kN + n) * kRows + lane];
-      float Bn[kTB], Cn[kTB];
+      for (int n = 0; n < kN; ++n) {
+        const bool nok = n < a.dstate;
+        const float A2n = a2s[n * kRows + lane];
+        const float An = A2n * kLn2;
+        const float x0n = (sub ? xmid : x0s)[n * kRows + lane];
+        const float* Bt = bcT + n * kTB + sub * kSub;
+        const float* Ct = bcT + (kN + n) * kTB + sub * kSub;
+        // forward sweep: states and decays of this sub-tile
+        float xs[kSub], as[kSub];
+        float x = x0n;
 #pragma unroll
-      for (int t4 = 0; t4 < kTB; t4 += 4) {
-        const float4 bq = *reinterpret_cast<const float4*>(bcT + n * kTB + t4);
-        const float4 cq = *reinterpret_cast<const float4*>(bcT + (kN + n) * kTB + t4);
-        Bn[t4] = bq.x; Bn[t4 + 1] = bq.y; Bn[t4 + 2] = bq.z; Bn[t4 + 3] = bq.w;
-        Cn[t4] = cq.x; Cn[t4 + 1] = cq.y; Cn[t4 + 2] = cq.z; Cn[t4 + 3] = cq.w;
-      }
-      const float An = A2n * kLn2;
-      // forward sweep: states and decays of this tile
-      float xs[kTB], as[kTB];
-      float x = x0n;
+        for (int t = 0; t < kSub; ++t) {
+          const float aa = fast_exp2(dt[t] * A2n);
+          x = fmaf(aa, x, dtu[t] * Bt[t]);
+          xs[t] = x;
+          as[t] = aa;
+          ys[t] = fmaf(Ct[t], x, ys[t]);
+        }
+        float red[kSub];
+        // dC_t,n = sum over the wave's channels of gy_t x_t,n
 #pragma unroll
-      for (int t = 0; t < kTB; ++t) {
-        const float aa = fast_exp2(dt[t] * A2n);
-        x = fmaf(aa, x, dt[t] * uu[t] * Bn[t]);
-        xs[t] = x;
-        as[t] = aa;
-        ys[t] = fmaf(Cn[t], x, ys[t]);
-      }
-      // reverse sweep
-      float h = lst[(2 * kN + n) * kRows + lane];
-      float red[32];
-      float dAn = 0.f;
+        for (int t = 0; t < kSub; ++t) red[t] = my_ok ? gy[t] * xs[t] : 0.f;
+        {
+          const float tot = wave_transpose_reduce<kSub>(red, lane);
+          const int t = lane / (64 / kSub);
+          if ((lane & (64 / kSub - 1)) == 0 && nok && p0 + t < L_)
+            a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 1) * L_ + p0 + t] = tot;
+        }
+        // reverse sweep
+        float h = carry[n * kRows + lane];
+        float dAn = 0.f;
 #pragma unroll
-      for (int t = kTB - 1; t >= 0; --t) {
-        h = fmaf(Cn[t], gy[t], h);
-        const float xp = t > 0 ? xs[t - 1] : x0n;
-        const float hdt = h * dt[t];
-        red[t] = hdt * uu[t];              // dB_t,n contribution
-        red[kTB + t] = gy[t] * xs[t];      // dC_t,n contribution
-        du[t] = fmaf(hdt, Bn[t], du[t]);
-        const float hax = h * as[t] * xp;
-        ddt[t] = fmaf(An, hax, fmaf(h * Bn[t], uu[t], ddt[t]));
-        dAn = fmaf(hax, dt[t], dAn);
-        h *= as[t];
-      }
-      lst[(2 * kN + n) * kRows + lane] = h;
-      lst[(3 * kN + n) * kRows + lane] += my_ok ? dAn : 0.f;
-      // channel sums of dB / dC for (n, 16 positions): lanes past the group end contribute 0
-      if (!my_ok) {
+        for (int t = kSub - 1; t >= 0; --t) {
+          h = fmaf(Ct[t], gy[t], h);
+          const float xp = t > 0 ? xs[t - 1] : x0n;
+          S[t] = fmaf(h, Bt[t], S[t]);
+          red[t] = my_ok ? h * dtu[t] : 0.f;              // dB_t,n contribution
+          const float ha = h * as[t];
+          const float hax = ha * xp;
+          Q[t] = fmaf(hax, An, Q[t]);
+          dAn = fmaf(hax, dt[t], dAn);
+          h = ha;
+        }
+        carry[n * kRows + lane] = h;
+        {
+          const float head = dAr[0] + dAn;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) red[i] = 0.f;
-      }
-      const float tot = wave_transpose_reduce32(red, lane);
-      if ((lane & 1) == 0 && n < a.dstate) {
-        const int k = lane >> 1;
-        const int which = k >> 4, t = k & 15;
-        if (l0 + t < L_)
-          a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + which) * L_ + l0 + t] = tot;
-      }
-    }
-
-    // ---- per-position outputs of my channel -> rows (fp32), then coalesced stores
-    {
-      float gz[kTB], sg[kTB];
-#pragma unroll
-      for (int t4 = 0; t4 < kTB; t4 += 4) {
-        const float4 a4 = *reinterpret_cast<const float4*>(prow + 2 * kTB + t4);
-        const float4 b4 = *reinterpret_cast<const float4*>(prow + 3 * kTB + t4);
-        gz[t4] = a4.x; gz[t4 + 1] = a4.y; gz[t4 + 2] = a4.z; gz[t4 + 3] = a4.w;
-        sg[t4] = b4.x; sg[t4 + 1] = b4.y; sg[t4 + 2] = b4.z; sg[t4 + 3] = b4.w;
-      }
-      float o_du[kTB], o_dd[kTB], o_dz[kTB];
-#pragma unroll
-      for (int t = 0; t < kTB; ++t) {
-        const bool live = l0 + t < L_;
-        const float y = fmaf(Dv, uu[t], ys[t]);
-        o_dz[t] = gz[t] * y;
-        o_du[t] = fmaf(Dv, gy[t], du[t]);
-        const float dr = ddt[t] * sg[t];
-        o_dd[t] = dr;
-        if (live && my_ok) {
-          dDacc = fmaf(gy[t], uu[t], dDacc);
-          dbacc += dr;
+          for (int k = 0; k < kN - 1; ++k) dAr[k] = dAr[k + 1];
+          dAr[kN - 1] = head;
+        }
+        {
+          const float tot = wave_transpose_reduce<kSub>(red, lane);
+          const int t = lane / (64 / kSub);
+          if ((lane & (64 / kSub - 1)) == 0 && nok && p0 + t < L_)
+            a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 0) * L_ + p0 + t] = tot;
         }
       }
+
+      // ---- per-position outputs of my channel (raw vectors re-read: L1/L2 hits)
+      {
+        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
+        load_raw(p0, full, ru, rd, rz, rg);
+        float o_du[kSub], o_dd[kSub], o_dz[kSub];
 #pragma unroll
-      for (int t4 = 0; t4 < kTB; t4 += 4) {
-        *reinterpret_cast<float4*>(prow + t4) = make_float4(o_du[t4], o_du[t4 + 1], o_du[t4 + 2], o_du[t4 + 3]);
-        *reinterpret_cast<float4*>(prow + kTB + t4) = make_float4(o_dd[t4], o_dd[t4 + 1], o_dd[t4 + 2], o_dd[t4 + 3]);
-        *reinterpret_cast<float4*>(prow + 2 * kTB + t4) = make_float4(o_dz[t4], o_dz[t4 + 1], o_dz[t4 + 2], o_dz[t4 + 3]);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kVPR; ++k) {
-      const int j = lane + k * kRows;
-      const int r = j / kVPR, c = j % kVPR;
-      if (r >= nrows) continue;
-      const int col0 = l0 + c * VI;
-      const int nv = max(0, min(VI, L_ - col0));
-      const float* src = reinterpret_cast<const float*>(rowbuf + r * RW::kStride);
-      const int64_t dd = dbase + r;
-#pragma unroll
-      for (int which = 0; which < 3; ++which) {
-        if (which == 2 && !hasZ) continue;
-        float v[VI];
-#pragma unroll
-        for (int e = 0; e < VI; ++e) v[e] = src[which * kTB + c * VI + e];
-        const int64_t off = which == 0   ? (int64_t)b * a.du_bs + dd * a.du_ds
-                            : which == 1 ? (int64_t)b * a.ddt_bs + dd * a.ddt_ds
-                                         : (int64_t)b * a.dz_bs + dd * a.dz_ds;
-        TI* dst = reinterpret_cast<TI*>(which == 0 ? a.du : (which == 1 ? a.ddelta : a.dz)) + off + col0;
-        const uint4 q = pack_f<TI>(v);
-        if (full) st16(dst, q);
-        else st16_masked(dst, q, nv);
+        for (int t = 0; t < kSub; ++t) {
+          float dtv, sgv, uv, gyv, gzv;
+          prep(rd, ru, rz, rg, p0, t, dtv, sgv, uv, gyv, gzv);
+          const float y = fmaf(Dv, uv, ys[t]);
+          o_dz[t] = gzv * y;
+          o_du[t] = fmaf(Dv, gyv, dtv * S[t]);
+          const float dr = fmaf(uv, S[t], Q[t]) * sgv;
+          o_dd[t] = dr;
+          if (p0 + t < L_ && my_ok) {
+            dDacc = fmaf(gyv, uv, dDacc);
+            dbacc += dr;
+          }
+        }
+        if (my_ok) {
+          store_row_sub<TI>(durow, p0, L_, full, o_du);
+          store_row_sub<TI>(ddrow, p0, L_, full, o_dd);
+          if (hasZ) store_row_sub<TI>(dzrow, p0, L_, full, o_dz);
+        }
       }
     }
   }
 
   if (my_ok) {
+    // slab_a is [b][n][d]: coalesced along d
 #pragma unroll
-    for (int n = 0; n < kN; ++n) a.slab_a[((int64_t)b * a.dim + my_d) * kN + n] = lst[(3 * kN + n) * kRows + lane];
+    for (int n = 0; n < kN; ++n) a.slab_a[((int64_t)b * kN + n) * a.dim + my_d] = dAr[n];
     a.slab_d[(int64_t)b * a.dim + my_d] = dDacc;
     a.slab_bias[(int64_t)b * a.dim + my_d] = dbacc;
   }
@@ -405,6 +429,28 @@ __global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__
   (void)out_cols;
 }
 
+// dA[d][n] = sum_b slab[b][n][d] (slab row stride ld): columns c = n * dim + d
+// (coalesced along d), output transposed to (dim, dstate).  Fixed-order sums.
+__global__ __launch_bounds__(256) void scan_bwd_colsum_nd(const float* __restrict__ in, int batch, int dim,
+                                                          int dstate, int64_t ld, float* __restrict__ out) {
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  const int cols = dim * dstate;
+  float s = 0.f;
+  if (c < cols)
+    for (int bb = q; bb < batch; bb += 8) s += in[(int64_t)bb * ld + c];
+  part[q][cx] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][cx];
+    const int n = c / dim, d = c % dim;
+    out[(int64_t)d * dstate + n] = t;
+  }
+}
+
 struct BwdWs {
   size_t bct, slab_bc, slab_a, slab_d, slab_bias, total;
 };
@@ -425,7 +471,7 @@ static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
 
 template <typename TI, int kN>
 static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
-  const size_t lds = (size_t)kRows * BwdRow<TI>::kStride + (size_t)2 * kN * kTB * 4 + (size_t)4 * kN * kRows * 4;
+  const size_t lds = (size_t)2 * kN * kTB * 4 + (size_t)4 * kN * kRows * 4;   // bcT + carry, xmid, x0s, a2s
   if (aligned)
     hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else
@@ -449,9 +495,10 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL((scan_bwd_reduce_bc<TW, kN>), dim3(grid), dim3(256), 0, s, a.slab_bc, a.batch, a.n_groups,
                      a.nblk, a.dstate, a.seqlen, reinterpret_cast<TW*>(dB), reinterpret_cast<TW*>(dC));
-  const int ca = a.dim * kN;
-  hipLaunchKernelGGL(scan_bwd_colsum, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, ca, (int64_t)ca,
-                     a.dim * a.dstate, kN, a.dstate, dA);
+  // slab_a is [b][n][d]: column c = n * dim + d -> dA[d][n] (transposed on output)
+  const int ca = a.dim * a.dstate;
+  hipLaunchKernelGGL(scan_bwd_colsum_nd, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, a.dim, a.dstate,
+                     (int64_t)a.dim * kN, dA);
   if (dD)
     hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_d, a.batch, a.dim,
                        (int64_t)a.dim, a.dim, 1, 1, dD);
