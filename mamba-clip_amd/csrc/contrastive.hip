@@ -27,7 +27,6 @@ namespace mc {
 namespace ctr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int BM = 128, BN = 128;
 constexpr int kRowBytes = 64;            // one K slice of a tile row

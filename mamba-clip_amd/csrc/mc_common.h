@@ -18,6 +18,10 @@ constexpr float kLn2 = 0.6931471805599453f;
 using bf16_t = __bf16;
 using f16_t = _Float16;
 
+// packed fp32 vectors: arithmetic on f32x2 lowers to v_pk_*_f32
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 template <typename T> struct ElemTraits;
 template <> struct ElemTraits<float> { static constexpr int kVec = 4; };   // 16 B = 4 elems
 template <> struct ElemTraits<bf16_t> { static constexpr int kVec = 8; };  // 16 B = 8 elems

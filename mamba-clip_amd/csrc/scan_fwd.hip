@@ -79,16 +79,19 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
   // ---- per-channel constants
   const int my_d = dbase + lane;
   const bool my_ok = lane < nrows;
-  float A2[kN];
+  // states are processed in pairs with packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32)
+  f32x2 A2[kN / 2];
 #pragma unroll
-  for (int n = 0; n < kN; ++n)
-    A2[n] = (my_ok && n < a.dstate) ? a.A[(int64_t)my_d * a.dstate + n] * kLog2e : 0.f;
+  for (int n = 0; n < kN; ++n) {
+    const float v = (my_ok && n < a.dstate) ? a.A[(int64_t)my_d * a.dstate + n] * kLog2e : 0.f;
+    if (n & 1) A2[n / 2].y = v; else A2[n / 2].x = v;
+  }
   const float Dv = (my_ok && a.D) ? a.D[my_d] : 0.f;
   const float biasv = (my_ok && a.delta_bias) ? a.delta_bias[my_d] : 0.f;
 
-  float x[kN];
+  f32x2 x[kN / 2];
 #pragma unroll
-  for (int n = 0; n < kN; ++n) x[n] = 0.f;
+  for (int n = 0; n < kN / 2; ++n) x[n] = f32x2{0.f, 0.f};
 
   // ---- register prefetch of the next chunk (issued before this chunk's
   // recurrence, consumed after it): u / delta vectors + the B/C chunk.
@@ -185,22 +188,24 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
           float dt = softplus ? softplus_f(dr) : dr;
           dt = (t < L_) ? dt : 0.f;  // past the end: state frozen
           const float du = dt * uv;
-          float y = 0.f;
+          f32x2 y2 = {0.f, 0.f};
           {
-            const float4* bc4 = reinterpret_cast<const float4*>(bcl + (t0 + e) * (2 * kN));
+            const f32x4* bc4 = reinterpret_cast<const f32x4*>(bcl + (t0 + e) * (2 * kN));
 #pragma unroll
             for (int n4 = 0; n4 < kN / 4; ++n4) {
-              const float4 bq = bc4[n4], cq = bc4[kN / 4 + n4];
-              const float bb[4] = {bq.x, bq.y, bq.z, bq.w}, cc[4] = {cq.x, cq.y, cq.z, cq.w};
+              const f32x4 bq = bc4[n4], cq = bc4[kN / 4 + n4];
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const float dA = fast_exp2(dt * A2[4 * n4 + i]);
-                x[4 * n4 + i] = fmaf(dA, x[4 * n4 + i], du * bb[i]);
-                y = fmaf(cc[i], x[4 * n4 + i], y);
+              for (int h = 0; h < 2; ++h) {
+                const int p = 2 * n4 + h;
+                const f32x2 bb = h ? bq.hi : bq.lo, cc = h ? cq.hi : cq.lo;
+                const f32x2 arg = A2[p] * dt;                               // v_pk_mul_f32
+                const f32x2 dA = {fast_exp2(arg.x), fast_exp2(arg.y)};
+                x[p] = dA * x[p] + bb * du;                                 // v_pk_mul + v_pk_fma
+                y2 = cc * x[p] + y2;                                        // v_pk_fma
               }
             }
           }
-          yv[e] = fmaf(Dv, uv, y);
+          yv[e] = fmaf(Dv, uv, y2.x + y2.y);
         }
         // y[0..kG/2) -> the u bytes, y[kG/2..kG) -> the delta bytes of this group
         if (a.chunk_states && my_ok && ((t0 + kG) % kS) == 0) {
@@ -211,11 +216,12 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
 #pragma unroll
               for (int n4 = 0; n4 < kN / 4; ++n4)
                 if (n4 * 4 < a.dstate)
-                  reinterpret_cast<float4*>(cs)[n4] = make_float4(x[4 * n4], x[4 * n4 + 1], x[4 * n4 + 2], x[4 * n4 + 3]);
+                  reinterpret_cast<float4*>(cs)[n4] =
+                      make_float4(x[2 * n4].x, x[2 * n4].y, x[2 * n4 + 1].x, x[2 * n4 + 1].y);
             } else {
 #pragma unroll
               for (int n = 0; n < kN; ++n)
-                if (n < a.dstate) cs[n] = x[n];
+                if (n < a.dstate) cs[n] = (n & 1) ? x[n / 2].y : x[n / 2].x;
             }
           }
         }
@@ -269,7 +275,7 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
     float* ls = a.last_state + ((int64_t)b * a.dim + my_d) * a.dstate;
 #pragma unroll
     for (int n = 0; n < kN; ++n)
-      if (n < a.dstate) ls[n] = x[n];
+      if (n < a.dstate) ls[n] = (n & 1) ? x[n / 2].y : x[n / 2].x;
   }
 }
 
