@@ -23,6 +23,8 @@
 //    y (+D u) is written back over the consumed row in fp32, and a
 //    cooperative pass applies the z gate with coalesced z loads / out stores.
 //  * exp(dt*A) = exp2(dt * A*log2e) on v_exp_f32.
+#include <cstdlib>
+
 #include "scan_common.h"
 
 
@@ -38,20 +40,18 @@ struct FwdArgs {
   void* out; float* chunk_states; float* last_state;
 };
 
-// waves per SIMD the register budget is sized for (16-bit I/O at dstate <= 16:
-// <= 128 VGPRs, no spill -> 4 waves/SIMD; wider variants get 2)
-// Register budget: 2 waves/SIMD (<= 256 VGPRs).  Measured on MI355X at C4
-// (B=64, D=3072, L=4096, N=16, bf16): 4-step groups at 2 waves/SIMD beat
-// 2-step groups at 3-4 waves/SIMD (the hoisted broadcast B/C reads of a
-// group need ~128 VGPRs) and the SGPR (scalar-load) B/C variant, whose
-// SGPR-operand VALU issues at ~0.6x the VGPR rate (tools/ubench/valu_rate.hip).
-template <typename TI, int kN>
-constexpr int fwd_min_waves() { return 2; }
-
-template <typename TI, int kN, bool kAligned>
-__global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_kernel(const FwdArgs a) {
+// Variants (template knobs, chosen on the host):
+//   kG     steps per group of the recurrence loop: the B/C values of a group
+//          are read from LDS together (kG * 2 * kN VGPRs live)
+//   kPBC   prefetch the next chunk's B/C into registers (else: load at staging)
+//   kPU    prefetch the next chunk's u / delta into registers (else: load at staging)
+//   kMinW  waves per SIMD the register budget is sized for
+// At C4 (B=64, D=3072: 3072 one-wave workgroups on 1024 SIMDs) the kernel is
+// VALU + v_exp issue bound (~33 SIMD cycles per wave per (t, n) step, measured
+// the same at 1 and 2 waves per SIMD), not HBM bound.
+template <typename TI, int kN, bool kAligned, int kG, bool kPBC, bool kPU, int kMinW>
+__global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a) {
   using RL = RowLayout<TI>;
-  constexpr int kG = 4;                         // steps per group in the recurrence loop
   constexpr int VI = RL::VI;                    // elements per 16-B vector
   constexpr int kVPR = kT / VI;                 // vectors per row segment per array
 
@@ -98,7 +98,16 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
   constexpr int kBCVec = kT * 2 * kN / 4;                 // float4s in one B/C chunk
   constexpr int kBCPer = (kBCVec + kRows - 1) / kRows;
   uint4 pu[kVPR], pd[kVPR];
-  float4 pbc[kBCPer];
+  float4 pbc[kPBC ? kBCPer : 1];
+  auto load_bc = [&](int l0, float4 (&dst)[kBCPer]) {
+    const float4* src = reinterpret_cast<const float4*>(a.bct + ((int64_t)bg * L_ + l0) * (2 * kN));
+    const int nvec = min(kT, L_ - l0) * (2 * kN) / 4;
+#pragma unroll
+    for (int k = 0; k < kBCPer; ++k) {
+      const int v = lane + k * kRows;
+      dst[k] = v < nvec ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
   auto load_regs = [&](int l0) {
     const bool full = kAligned && (l0 + kT <= L_);
 #pragma unroll
@@ -118,21 +127,14 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
         pd[k] = ld16_masked(sd, nv);
       }
     }
-    {
-      const float4* src = reinterpret_cast<const float4*>(a.bct + ((int64_t)bg * L_ + l0) * (2 * kN));
-      const int nvec = min(kT, L_ - l0) * (2 * kN) / 4;
-#pragma unroll
-      for (int k = 0; k < kBCPer; ++k) {
-        const int v = lane + k * kRows;
-        pbc[k] = v < nvec ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
+    if constexpr (kPBC) load_bc(l0, pbc);
   };
 
-  load_regs(0);
+  if constexpr (kPU) load_regs(0);
   for (int ch = 0; ch < a.n_chunks; ++ch) {
     const int l0 = ch * kT;
     const bool full = kAligned && (l0 + kT <= L_);
+    if constexpr (!kPU) load_regs(l0);   // other resident waves cover the latency
 
     // ---- stage u / delta (vector j = lane + k*64 -> row j / kVPR, col j % kVPR) and B/C
 #pragma unroll
@@ -144,14 +146,23 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
       st16(blk + 16, pd[k]);
     }
     {
+      float4 cur[kBCPer];
+      if constexpr (kPBC) {
+#pragma unroll
+        for (int k = 0; k < kBCPer; ++k) cur[k] = pbc[k];
+      } else {
+        load_bc(l0, cur);   // L2-resident (shared by the waves of this batch); latency once per chunk
+      }
 #pragma unroll
       for (int k = 0; k < kBCPer; ++k) {
         const int v = lane + k * kRows;
-        if (v < kBCVec) reinterpret_cast<float4*>(bcl)[v] = pbc[k];
+        if (v < kBCVec) reinterpret_cast<float4*>(bcl)[v] = cur[k];
       }
     }
     __syncthreads();
-    if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
+    if constexpr (kPU) {
+      if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
+    }
 
     // ---- the recurrence over this chunk, one channel per lane.  Steps go
     // in groups of kG: read the group's u / delta (kG elements each), run
@@ -280,16 +291,40 @@ __global__ __launch_bounds__(kRows, (fwd_min_waves<TI, kN>())) void scan_fwd_ker
 }
 
 // ------------------------------------------------------------------ host dispatch
-template <typename TI, int kN>
-static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
+template <typename TI, int kN, int kG, bool kPBC, bool kPU, int kMinW>
+static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
   const size_t lds = (size_t)kRows * RowLayout<TI>::kStride + (size_t)kT * 2 * kN * 4;
   if (aligned)
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, true, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, false>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, false, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s,
+                       a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
+}
+
+// MC_SCAN_FWD_VARIANT (development A/B only; measured on MI355X, C4 / B=42 / C2 fwd):
+//   0 = kG 4, u/delta + B/C prefetch, 2 waves/SIMD       3.38 / 2.16 / 0.204 ms (default)
+//   2 = kG 2, u/delta + B/C prefetch, 2 waves/SIMD       3.44 / 2.23 / 0.209 ms
+//   3 = kG 2, no prefetch, 3 waves/SIMD (147 VGPRs)      4.31 / 2.92 / 0.195 ms
+// Three resident waves per SIMD remove the half-empty second round at C4 but
+// run each (t, n) ~1.3x slower, so the 2-wave variant stays the default.
+static int fwd_variant() {
+  static const int v = [] {
+    const char* e = getenv("MC_SCAN_FWD_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <typename TI, int kN>
+static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
+  switch (fwd_variant()) {
+    case 2: return launch_fwd_v<TI, kN, 2, true, true, 2>(a, aligned, s);
+    case 3: return launch_fwd_v<TI, kN, 2, false, false, 3>(a, aligned, s);
+    default: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
+  }
 }
 
 template <typename TI>
