@@ -17,6 +17,7 @@ over the fp32 logits -- no host sync, no eager softmax.
 """
 import torch
 import torch.distributed as dist
+import torch.distributed.nn  # noqa: F401  (gather_with_grad; the reference forgets it: SURVEY Appendix A.4)
 import torch.nn.functional as F
 
 from .ops import gemm_nt, scaled_logits_ce
@@ -53,7 +54,6 @@ def all_gather(image_features, text_features, local_loss=False, gather_with_grad
     (unless local_loss, where the gathered copies stay gradient-free).
     """
     if gather_with_grad:
-        import torch.distributed.nn  # noqa: F401  (the reference forgets this import: SURVEY Appendix A.4)
         all_image = torch.cat(torch.distributed.nn.all_gather(image_features), dim=0)
         all_text = torch.cat(torch.distributed.nn.all_gather(text_features), dim=0)
         return all_image, all_text

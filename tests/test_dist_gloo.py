@@ -83,3 +83,80 @@ def test_clip_loss_distributed_matches_reference(world):
         p.join(timeout=60)
     for rank, res in results.items():
         assert all(res.values()), f"rank {rank}: {res}"
+
+
+# ---------------------------------------------------------------- DDP train step (train.py step semantics)
+def _ddp_worker(rank, world, port, q):
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+        from types import SimpleNamespace
+        import torch.distributed as dist
+        import mamba_clip_amd.loss as L
+        from mamba_clip_amd.model import build_clip
+        from mamba_clip_amd.train import create_optimizer, train_step, wrap_ddp
+        from oracle.cpu_model import oracle_ops
+        L.scaled_logits_ce = _cpu_scaled_logits_ce
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        args = SimpleNamespace(precision="fp32", lr=1e-3, wd=0.1, beta1=0.9, beta2=0.98, eps=1e-8,
+                               grad_clip_norm=None, distributed=True, ddp_static_graph=False, rank=rank,
+                               world_size=world)
+        g = torch.Generator().manual_seed(5)
+        B = 4 * world
+        images = torch.randn(B, 3, 32, 32, generator=g)
+        texts = torch.randint(1, 999, (B, 16), generator=g)
+        texts[:, -1] = 999
+        targets = torch.zeros(B, dtype=torch.long)
+        sl = slice(rank * 4, (rank + 1) * 4)
+        with oracle_ops():
+            torch.manual_seed(0)
+            model = wrap_ddp(build_clip("tiny-mamba-clip"), args, torch.device("cpu"))
+            loss = L.ClipLoss(rank=rank, world_size=world)
+            # gradients: DDP averages the per-rank gradients of the GLOBAL loss w.r.t. the local
+            # features, so world * grad == the single-process gradient on the whole batch
+            out = model(images[sl], texts[sl])
+            loss(**out)["contrastive_loss"].backward()
+            grads = torch.cat([p.grad.flatten() for p in model.module.parameters()]) * world
+            opt = create_optimizer(model, args)
+            train_step(model, images[sl], texts[sl], targets[sl], loss, opt, None, args)
+            params = torch.cat([p.detach().flatten() for p in model.module.parameters()])
+            res = {"params": params.numpy(), "grads": grads.numpy()}
+            if rank == 0:   # single process on the whole global batch, same init
+                torch.manual_seed(0)
+                ref = build_clip("tiny-mamba-clip")
+                ref_out = ref(images, texts)
+                L.ClipLoss()(**ref_out)["contrastive_loss"].backward()
+                res["ref_grads"] = torch.cat([p.grad.flatten() for p in ref.parameters()]).numpy()
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+def test_ddp_train_step_matches_single_process_gloo_w2():
+    """wrap_ddp + ClipLoss(rank, world) + train_step on 2 gloo ranks == one process on the global batch."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+    np.testing.assert_array_equal(out[0]["params"], out[1]["params"])          # replicas stay identical
+    np.testing.assert_array_equal(out[0]["grads"], out[1]["grads"])            # all-reduced gradients
+    # every rank evaluates the full global loss, so the shared logit_scale (parameter 0 of ClipModel:
+    # registered first) gets the FULL gradient after DDP averaging, the towers 1/world of it
+    # (the reference's semantics as well)
+    g, ref = out[0]["grads"], out[0]["ref_grads"]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(g[1:], ref[1:], rtol=1e-4, atol=1e-6 * scale)
+    np.testing.assert_allclose(g[0] / world, ref[0], rtol=1e-4)

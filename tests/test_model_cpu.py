@@ -53,3 +53,34 @@ def test_cpu_restatement_train_step_runs():
     from oracle.cpu_model import cpu_train_pairs_per_sec
     pps, secs = cpu_train_pairs_per_sec("tiny-mamba-clip", batch=4, steps=1, warmup=1)
     assert pps > 0 and secs > 0
+
+
+def test_cli_parser_hot_path_flags():
+    from mamba_clip_amd.cli import build_parser
+    a = build_parser().parse_args(["--synthetic", "--batch-size", "8", "--local-loss", "--gather-with-grad",
+                                   "--lr-scheduler", "const", "--stage", "2", "--use-inner-prod", "--accum-freq", "2"])
+    assert a.synthetic and a.local_loss and a.gather_with_grad and a.stage == 2 and a.use_inner_prod
+    assert a.precision == "amp_bf16" and a.accum_freq == 2 and a.model == "vit_b16-mamba130m"
+
+
+def test_cli_requires_synthetic():
+    import pytest
+    from mamba_clip_amd.cli import main
+    with pytest.raises(SystemExit):
+        main(["--batch-size", "4"])
+
+
+def test_schedulers_match_reference_formulas():
+    import math
+    from mamba_clip_amd.scheduler import const_lr, const_lr_cooldown, cosine_lr
+
+    class Opt:
+        param_groups = [{"lr": 0.0}]
+    o = Opt()
+    f = cosine_lr(o, 1.0, 10, 110)
+    assert abs(f(0) - 0.1) < 1e-12 and abs(f(9) - 1.0) < 1e-12
+    assert abs(f(60) - 0.5 * (1 + math.cos(math.pi * 50 / 100))) < 1e-12
+    g = const_lr(o, 2.0, 4, 100)
+    assert g(1) == 1.0 and g(50) == 2.0
+    h = const_lr_cooldown(o, 1.0, 0, 100, 20, cooldown_power=1.0, cooldown_end_lr=0.0)
+    assert h(79) == 1.0 and abs(h(90) - 0.5) < 1e-12 and o.param_groups[0]["lr"] == h(90)

@@ -265,3 +265,15 @@ def test_tiny_clip_train_step():
         assert torch.allclose(out["image_features"].float().norm(dim=-1), torch.ones(8, device=DEV), atol=1e-2)
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]          # it learns the (fixed) batch
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_cli_synthetic_tiny(stage, capsys):
+    from mamba_clip_amd.cli import main
+    rc = main(["--synthetic", "--model", "tiny-mamba-clip", "--batch-size", "8", "--train-num-samples", "24",
+               "--stage", str(stage), "--benchmark", "--log-every-n-steps", "1", "--warmup", "1"])
+    assert rc == 0
+    import json
+    line = [l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["pairs_per_sec"] > 0 and out["final"]["loss"] is not None
