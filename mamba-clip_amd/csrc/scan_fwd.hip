@@ -290,6 +290,256 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   }
 }
 
+typedef __attribute__((address_space(4))) const f32x4 cf32x4;   // constant address space: scalar loads
+
+// Row layout of the 16-position chunk variants: per row {u vector, delta vector} blocks + 16-B pad.
+template <typename TI>
+struct RowLayoutP {
+  static constexpr int kTP = 16;
+  static constexpr int VI = ElemTraits<TI>::kVec;
+  static constexpr int kBlock = 32;                 // {u vector, delta vector}
+  static constexpr int kBlocks = kTP / VI;
+  static constexpr int kStride = kBlocks * kBlock + 16;
+};
+
+// ------------------------------------------------------------------ multi-channel-per-lane variant
+// kR channels per lane (a wave owns 64*kR channels of one (batch, group)):
+// the kR recurrences are independent, so they interleave in one instruction
+// stream and hide each other's latencies (ILP instead of resident waves), and
+// each position's B/C row -- loaded once per wave into SGPRs -- serves kR
+// times the work.  At C4 (B=64, D=3072) kR = 3 gives 1024 waves: exactly one
+// per SIMD, no tail round.  u / delta / z of the next chunk are prefetched
+// into registers during the current chunk (z too: the gate pass never waits
+// on HBM).
+template <typename TI, int kN, int kR, bool kAligned, bool kSP>
+__global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(const FwdArgs a) {
+  using RL = RowLayoutP<TI>;
+  constexpr int kTP = RL::kTP;
+  constexpr int VI = RL::VI;
+  constexpr int kVPR = kTP / VI;                  // vectors per row per array
+  constexpr int kQ = kN / 4;
+  constexpr int kW = kRows * kR;                  // channels per wave
+  constexpr int kVL = kR * kVPR;                  // staged vectors per lane per array
+  static_assert(kTP % kS == 0, "chunk-state positions must be static within a chunk");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* rowbuf = smem;                            // [kW][RL::kStride]
+
+  const int lane = threadIdx.x;
+  const int lin = xcd_remap(blockIdx.x, a.total_blocks);
+  const int dblk = lin % a.nblk;
+  const int bg = lin / a.nblk;
+  const int g = bg % a.n_groups, b = bg / a.n_groups;
+  const int H = a.dim / a.n_groups;
+  const int dbase = g * H + dblk * kW;
+  const int nrows = min(kW, H - dblk * kW);
+  const int L_ = a.seqlen;
+  const bool hasZ = a.z != nullptr;
+  const int n_chunks = (L_ + kTP - 1) / kTP;
+
+  const TI* __restrict__ u = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs;
+  const TI* __restrict__ dl = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs;
+  const TI* __restrict__ zp = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs;
+  TI* __restrict__ out = reinterpret_cast<TI*>(a.out) + (int64_t)b * a.o_bs;
+  const cf32x4* bcs = (const cf32x4*)(a.bct + (int64_t)bg * L_ * (2 * kN));
+
+  // channel r of this lane: row lane + 64 r of the wave's block
+  f32x2 A2[kR][kN / 2], x[kR][kN / 2];
+  float Dv[kR], biasv[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int row = lane + kRows * r;
+    const bool ok = row < nrows;
+    const int d = dbase + min(row, nrows - 1);
+#pragma unroll
+    for (int n = 0; n < kN; ++n) {
+      const float v = (ok && n < a.dstate) ? a.A[(int64_t)d * a.dstate + n] * kLog2e : 0.f;
+      if (n & 1) A2[r][n / 2].y = v; else A2[r][n / 2].x = v;
+    }
+    Dv[r] = (ok && a.D) ? a.D[d] : 0.f;
+    biasv[r] = (ok && a.delta_bias) ? a.delta_bias[d] : 0.f;
+#pragma unroll
+    for (int p = 0; p < kN / 2; ++p) x[r][p] = f32x2{0.f, 0.f};
+  }
+
+  // staged vector k of this lane: j = lane + 64 k -> row j / kVPR, column block j % kVPR
+  uint4 pu[kVL], pd[kVL], pz[kVL];
+  auto load_regs = [&](int l0) {
+    const bool full = kAligned && (l0 + kTP <= L_);
+#pragma unroll
+    for (int k = 0; k < kVL; ++k) {
+      const int j = lane + k * kRows;
+      const int r = j / kVPR, c = j % kVPR;
+      const int rr = min(r, nrows - 1);
+      const int col0 = l0 + c * VI;
+      const TI* su = u + (int64_t)(dbase + rr) * a.u_ds + col0;
+      const TI* sd = dl + (int64_t)(dbase + rr) * a.dt_ds + col0;
+      const TI* sz = zp + (int64_t)(dbase + rr) * a.z_ds + col0;
+      if (full) {
+        pu[k] = ld16(su);
+        pd[k] = ld16(sd);
+        if (hasZ) pz[k] = ld16(sz);
+      } else {
+        const int nv = max(0, min(VI, L_ - col0));
+        pu[k] = ld16_masked(su, nv);
+        pd[k] = ld16_masked(sd, nv);
+        if (hasZ) pz[k] = ld16_masked(sz, nv);
+      }
+    }
+  };
+  auto load_bc = [&](int t, f32x4 (&dst)[2 * kQ]) {
+    const cf32x4* src = bcs + (int64_t)min(t, L_ - 1) * (2 * kQ);
+#pragma unroll
+    for (int k = 0; k < 2 * kQ; ++k) dst[k] = src[k];
+  };
+
+  f32x4 bcA[2 * kQ], bcB[2 * kQ];
+  load_bc(0, bcA);
+  load_regs(0);
+  for (int ch = 0; ch < n_chunks; ++ch) {
+    const int l0 = ch * kTP;
+    const bool full = kAligned && (l0 + kTP <= L_);
+#pragma unroll
+    for (int k = 0; k < kVL; ++k) {
+      const int j = lane + k * kRows;
+      const int r = j / kVPR, c = j % kVPR;
+      char* blk = rowbuf + r * RL::kStride + c * RL::kBlock;
+      st16(blk, pu[k]);
+      st16(blk + 16, pd[k]);
+    }
+    uint4 cz[kVL];
+#pragma unroll
+    for (int k = 0; k < kVL; ++k) cz[k] = pz[k];
+    __syncthreads();
+    uint4 ru[kR][kVPR], rd[kR][kVPR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const char* rowp = rowbuf + (lane + kRows * r) * RL::kStride;
+#pragma unroll
+      for (int k = 0; k < kVPR; ++k) {
+        ru[r][k] = ld16(rowp + k * RL::kBlock);
+        rd[r][k] = ld16(rowp + k * RL::kBlock + 16);
+      }
+    }
+    if (ch + 1 < n_chunks) load_regs(l0 + kTP);
+
+    auto step = [&](int tt, const f32x4 (&cur)[2 * kQ], f32x4 (&nxt)[2 * kQ]) {
+      const int t = l0 + tt;
+      __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0): cur (issued a position ago) is back
+      __builtin_amdgcn_sched_barrier(0);
+      load_bc(t + 1, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const float uv = elem_f<TI>(ru[r][tt / VI], tt % VI);
+        const float dr = elem_f<TI>(rd[r][tt / VI], tt % VI) + biasv[r];
+        float dt = kSP ? softplus_f(dr) : dr;   // template flag: no per-position branch
+        dt = (t < L_) ? dt : 0.f;
+        const float du = dt * uv;
+        f32x2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+          const f32x4 bq = cur[q], cq = cur[kQ + q];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int p = 2 * q + h;
+            const f32x2 bb = h ? bq.hi : bq.lo, cc = h ? cq.hi : cq.lo;
+            const f32x2 arg = A2[r][p] * dt;
+            const f32x2 dA = {fast_exp2(arg.x), fast_exp2(arg.y)};
+            x[r][p] = dA * x[r][p] + bb * du;
+            if (h) yb = cc * x[r][p] + yb;
+            else ya = cc * x[r][p] + ya;
+          }
+        }
+        const f32x2 ys = ya + yb;
+        reinterpret_cast<float*>(rowbuf + (lane + kRows * r) * RL::kStride)[tt] = fmaf(Dv[r], uv, ys.x + ys.y);
+        const int row = lane + kRows * r;
+        if (((tt + 1) % kS) == 0 && a.chunk_states && row < nrows) {
+          const int sc = (t + 1) / kS - 1;
+          if (sc < a.n_states) {
+            float* cs = a.chunk_states + (((int64_t)b * a.dim + dbase + row) * a.n_states + sc) * a.dstate;
+            if ((a.dstate & 3) == 0) {
+#pragma unroll
+              for (int n4 = 0; n4 < kN / 4; ++n4)
+                if (n4 * 4 < a.dstate)
+                  reinterpret_cast<float4*>(cs)[n4] =
+                      make_float4(x[r][2 * n4].x, x[r][2 * n4].y, x[r][2 * n4 + 1].x, x[r][2 * n4 + 1].y);
+            } else {
+#pragma unroll
+              for (int n = 0; n < kN; ++n)
+                if (n < a.dstate) cs[n] = (n & 1) ? x[r][n / 2].y : x[r][n / 2].x;
+            }
+          }
+        }
+      }
+    };
+#pragma unroll
+    for (int tt = 0; tt < kTP; tt += 2) {
+      step(tt, bcA, bcB);
+      step(tt + 1, bcB, bcA);
+    }
+    __syncthreads();
+
+    // ---- gate + store, coalesced along the sequence (z prefetched a chunk ago)
+#pragma unroll
+    for (int k = 0; k < kVL; ++k) {
+      const int j = lane + k * kRows;
+      const int r = j / kVPR, c = j % kVPR;
+      const int col0 = l0 + c * VI;
+      const int nv = max(0, min(VI, L_ - col0));
+      float o[VI];
+      const float4* yv = reinterpret_cast<const float4*>(rowbuf + r * RL::kStride + c * VI * 4);
+#pragma unroll
+      for (int e4 = 0; e4 < VI / 4; ++e4) {
+        const float4 q = yv[e4];
+        o[4 * e4] = q.x; o[4 * e4 + 1] = q.y; o[4 * e4 + 2] = q.z; o[4 * e4 + 3] = q.w;
+      }
+      if (hasZ) {
+#pragma unroll
+        for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(cz[k], e));
+      }
+      if (r < nrows) {
+        TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
+        const uint4 ov = pack_f<TI>(o);
+        if (full) st16(dst, ov);
+        else st16_masked(dst, ov, nv);
+      }
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int row = lane + kRows * r;
+    if (a.last_state && row < nrows) {
+      float* ls = a.last_state + ((int64_t)b * a.dim + dbase + row) * a.dstate;
+#pragma unroll
+      for (int n = 0; n < kN; ++n)
+        if (n < a.dstate) ls[n] = (n & 1) ? x[r][n / 2].y : x[r][n / 2].x;
+    }
+  }
+}
+
+template <typename TI, int kN, int kR>
+static int launch_fwd_mc(const FwdArgs& a0, bool aligned, hipStream_t s) {
+  FwdArgs a = a0;
+  const int H = a.dim / a.n_groups;
+  a.nblk = (H + kRows * kR - 1) / (kRows * kR);
+  a.total_blocks = a.batch * a.n_groups * a.nblk;
+  const size_t lds = (size_t)kRows * kR * RowLayoutP<TI>::kStride;
+  if (aligned && a.softplus)
+    hipLaunchKernelGGL((scan_fwd_mc_kernel<TI, kN, kR, true, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  else if (aligned)
+    hipLaunchKernelGGL((scan_fwd_mc_kernel<TI, kN, kR, true, false>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  else if (a.softplus)
+    hipLaunchKernelGGL((scan_fwd_mc_kernel<TI, kN, kR, false, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  else
+    hipLaunchKernelGGL((scan_fwd_mc_kernel<TI, kN, kR, false, false>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <typename TI, int kN, int kG, bool kPBC, bool kPU, int kMinW>
 static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
@@ -304,25 +554,32 @@ static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
   return MC_OK;
 }
 
-// MC_SCAN_FWD_VARIANT (development A/B only; measured on MI355X, C4 / B=42 / C2 fwd):
-//   0 = kG 4, u/delta + B/C prefetch, 2 waves/SIMD       3.38 / 2.16 / 0.204 ms (default)
-//   2 = kG 2, u/delta + B/C prefetch, 2 waves/SIMD       3.44 / 2.23 / 0.209 ms
-//   3 = kG 2, no prefetch, 3 waves/SIMD (147 VGPRs)      4.31 / 2.92 / 0.195 ms
-// Three resident waves per SIMD remove the half-empty second round at C4 but
-// run each (t, n) ~1.3x slower, so the 2-wave variant stays the default.
+// Kernel choice, measured on MI355X (tools/ab_scan_fwd.sh; ms, bf16, z, softplus):
+//                                         C4 64x3072x4096   C2 256x1536x80
+//   scan_fwd_kernel (kG 4, LDS B/C, 2 w/SIMD)     3.35             0.204
+//   scan_fwd_mc_kernel R=1 (SGPR B/C, 16-pos)     3.87             0.152
+//   scan_fwd_mc_kernel R=3 (1 w/SIMD)             3.66             0.180
+// Rejected (kept in git history): per-position LDS broadcast at 3 w/SIMD
+// 3.96 / 0.188; two-wave state split with SGPR half-rows 6.41 / 0.266;
+// vector-load B/C rings spill at the occupancy they need.  With short
+// sequences the grid is many short-lived waves and the SGPR-fed kernel wins;
+// with long ones the LDS-staged kernel's deeper prefetch wins.
+// MC_SCAN_FWD_VARIANT overrides the choice for A/B runs: 0 = LDS-staged, 10 = SGPR R=1, 8 = SGPR R=3.
 static int fwd_variant() {
   static const int v = [] {
     const char* e = getenv("MC_SCAN_FWD_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
   return v;
 }
 
 template <typename TI, int kN>
 static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
-  switch (fwd_variant()) {
-    case 2: return launch_fwd_v<TI, kN, 2, true, true, 2>(a, aligned, s);
-    case 3: return launch_fwd_v<TI, kN, 2, false, false, 3>(a, aligned, s);
+  int v = fwd_variant();
+  if (v < 0) v = a.seqlen <= 512 ? 10 : 0;
+  switch (v) {
+    case 8: return launch_fwd_mc<TI, kN, 3>(a, aligned, s);
+    case 10: return launch_fwd_mc<TI, kN, 1>(a, aligned, s);
     default: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
   }
 }
