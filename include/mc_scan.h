@@ -53,7 +53,7 @@ enum {
 #define MC_SCAN_MAX_DSTATE 32
 /* sequence positions per saved chunk state (training forward writes the state
  * after every MC_SCAN_CHUNK positions; the backward resumes from them) */
-#define MC_SCAN_CHUNK 16
+#define MC_SCAN_CHUNK 8
 
 typedef struct mc_scan_fwd_params {
   int32_t batch, dim, seqlen, dstate, n_groups;

@@ -11,28 +11,28 @@
 //   dA_n  = sum_{b,t} h_t,n dt_t a_t,n x_{t-1,n}    dD = sum gy u    dbias = sum ddelta
 //
 // Design (DESIGN.md "scan_bwd"):
-//  * one wave = 64 channels of one (batch, group); tiles of kS = 16 positions
-//    walked in reverse; each tile restarts from the fp32 state the training
-//    forward saved at its start (chunk_states), so nothing is recomputed
-//    across tiles.
-//  * each lane reads / writes its own row's positions as 16-B vectors (no
-//    LDS staging of the rows).  LDS holds the B/C tile and the per-lane,
-//    per-state scalars (A, tile-start state, mid-tile state, adjoint carry;
-//    18 KB per wave at dstate 16) so the n-loop never waits on global memory.
-//  * the n-loop runs on 8-position sub-tiles (register budget); the state at
-//    the middle of a 16-position tile is recomputed from the saved tile-start
-//    state by a short forward pre-pass.
-//  * inside a tile the state index n is the outer loop: a forward sweep keeps
-//    x_t,n and a_t,n for the 16 positions in VGPRs, the reverse sweep consumes
-//    them; per-position accumulators stay in VGPRs across n:
+//  * one wave = 64 channels of one (batch, group); tiles of kTB = kS = 8
+//    positions walked in reverse; each tile restarts from the fp32 state the
+//    training forward saved at its start (chunk_states), so nothing is
+//    recomputed across tiles and no mid-tile pre-pass is needed.
+//  * state pairs (n, n+1) in packed fp32; the pair loop is fully unrolled, so
+//    A, the adjoint carry and the dA accumulators of every pair stay in VGPRs.
+//    Per pair and tile: a forward sweep (x, a kept in VGPRs), the reverse
+//    adjoint sweep; per-position accumulators carried across pairs:
 //      S_t = sum_n h B,  Q_t = sum_n h A a x_{t-1},  y_t = sum_n C x
-//    so du = dt S + D gy and ddt = Q + u S need no per-n work.
+//    so du = dt S + D gy and ddt = (Q + u S) sigmoid need no per-n work.
+//  * each lane reads / writes its own row's positions as 16-B vectors; the
+//    next tile's rows, B/C quads and saved state are prefetched into
+//    registers under the current tile.  The tile's B/C block sits in LDS as
+//    [pair][position]{B_n, B_n+1, C_n, C_n+1}: one broadcast ds_read_b128.
 //  * dB/dC (sums over the 64 channels of the wave) use an in-register
 //    transpose-reduce: permlane32_swap / permlane16_swap / DPP row_ror:8 /
 //    ds_swizzle / quad_perm halving stages turn 16 per-lane values into 16
-//    wave sums in ~2 VALU per value, then land in a per-wave fp32 slab.  A
+//    wave sums in ~2.5 VALU per value, then land in a per-wave fp32 slab.  A
 //    small second kernel sums the slabs over waves / batches: deterministic,
 //    no atomics.
+#include <cstdlib>
+
 #include "scan_common.h"
 
 namespace mc {
@@ -55,14 +55,19 @@ struct BwdArgs {
 };
 
 __device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
-  // ctrl_sel: 0 -> row_ror:8 (xor 8), 1 -> ds_swizzle xor 4, 2 -> quad_perm[2,3,0,1] (xor 2),
+  // ctrl_sel: 0 -> row_ror:8 (xor 8), 1 -> xor 4 (row_shl/shr:4 by bank), 2 -> quad_perm[2,3,0,1] (xor 2),
   // 3 -> quad_perm[1,0,3,2] (xor 1).  Every partner is lane ^ bit exactly: the
   // halving stages need partners that agree on the bits already reduced
   // (row_ror:4 is NOT xor 4 -- it can flip bit 3; tools/ubench/reduce_check.hip).
   const int iv = __float_as_int(v);
   int r;
   if (ctrl_sel == 0) r = __builtin_amdgcn_update_dpp(iv, iv, 0x128, 0xF, 0xF, false);
-  else if (ctrl_sel == 1) r = __builtin_amdgcn_ds_swizzle(iv, 0x101F);  // bitmask mode: and 0x1F, xor 4
+  else if (ctrl_sel == 1) {
+    // xor 4 inside each 16-lane row, on the VALU (no LDS, so no lgkmcnt wait):
+    // banks 0/2 (lanes 0-3, 8-11) take lane + 4 (row_shl:4), banks 1/3 take lane - 4 (row_shr:4)
+    const int lo = __builtin_amdgcn_update_dpp(iv, iv, 0x104, 0xF, 0x5, false);
+    r = __builtin_amdgcn_update_dpp(lo, iv, 0x114, 0xF, 0xA, false);
+  }
   else if (ctrl_sel == 2) r = __builtin_amdgcn_update_dpp(iv, iv, 0x4E, 0xF, 0xF, false);
   else r = __builtin_amdgcn_update_dpp(iv, iv, 0xB1, 0xF, 0xF, false);
   return __int_as_float(r);
@@ -109,17 +114,15 @@ __device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane)
   return v[0] + dpp_f(v[0], 3);         // lane bit 0 via quad_perm [1,0,3,2]
 }
 
-constexpr int kSub = kTB / 2;            // positions per sub-tile of the n-loop (8)
-
-// Own-row vector I/O: a lane reads / writes kSub consecutive positions of its
-// own (b, d) row as 16-B vectors (no LDS staging: a wave revisits its rows
-// tile after tile, so L2 sees whole lines).
+// Own-row vector I/O: a lane reads / writes the kTB consecutive positions of
+// its own (b, d) row as 16-B vectors (no LDS staging of the rows: a wave
+// revisits its rows tile after tile, so L2 sees whole lines).
 template <typename TI>
-__device__ __forceinline__ void load_row_sub(const TI* __restrict__ p, int l0, int L, bool full,
-                                             uint4 (&q)[kSub / ElemTraits<TI>::kVec]) {
+__device__ __forceinline__ void load_row_tile(const TI* __restrict__ p, int l0, int L, bool full,
+                                              uint4 (&q)[kTB / ElemTraits<TI>::kVec]) {
   constexpr int VI = ElemTraits<TI>::kVec;
 #pragma unroll
-  for (int k = 0; k < kSub / VI; ++k) {
+  for (int k = 0; k < kTB / VI; ++k) {
     const int col0 = l0 + k * VI;
     if (full) q[k] = ld16(p + col0);
     else q[k] = ld16_masked(p + col0, max(0, min(VI, L - col0)));
@@ -127,10 +130,10 @@ __device__ __forceinline__ void load_row_sub(const TI* __restrict__ p, int l0, i
 }
 
 template <typename TI>
-__device__ __forceinline__ void store_row_sub(TI* __restrict__ p, int l0, int L, bool full, const float (&v)[kSub]) {
+__device__ __forceinline__ void store_row_tile(TI* __restrict__ p, int l0, int L, bool full, const float (&v)[kTB]) {
   constexpr int VI = ElemTraits<TI>::kVec;
 #pragma unroll
-  for (int k = 0; k < kSub / VI; ++k) {
+  for (int k = 0; k < kTB / VI; ++k) {
     float w[VI];
 #pragma unroll
     for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
@@ -140,17 +143,33 @@ __device__ __forceinline__ void store_row_sub(TI* __restrict__ p, int l0, int L,
   }
 }
 
+// One wave = 64 channels of one (batch, group); tiles of kTB = 8 positions in
+// reverse; state PAIRS (n, n+1) are the unit of work, in packed fp32
+// (v_pk_mul_f32 / v_pk_fma_f32), fully unrolled over the kN / 2 pairs so the
+// per-pair lane constants (A, the adjoint carry, the dA accumulator) live in
+// VGPRs.  Per pair and tile: a forward sweep from the saved tile-start state
+// (decays and states kept in VGPRs), the dC contributions reduced across the
+// wave, then the reverse adjoint sweep and the dB reduction.  The tile's B/C
+// block is staged in LDS as [pair][position]{B_n, B_n+1, C_n, C_n+1} so one
+// broadcast ds_read_b128 serves a (pair, position).  The next tile's rows,
+// B/C block and saved state are prefetched into registers under this tile.
 template <typename TI, int kN, bool kAligned>
 __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   constexpr int VI = ElemTraits<TI>::kVec;
-  constexpr int kVPS = kSub / VI;   // 16-B vectors per sub-tile of one row (1 for 16-bit, 2 for fp32)
+  constexpr int kVT = kTB / VI;            // 16-B vectors per row tile (1 for 16-bit, 2 for fp32)
+  constexpr int kP = kN / 2;               // state pairs
+  constexpr int kBCQ = kP * kTB;           // (pair, position) quads of one tile
+  constexpr int kBCPer = (kBCQ + kRows - 1) / kRows;
 
   extern __shared__ __attribute__((aligned(16))) float smem_f[];
-  float* bcT = smem_f;                   // [2kN][kTB]: B rows then C rows of this tile
-  float* carry = bcT + 2 * kN * kTB;     // [kN][kRows]: adjoint carried into the previous positions
-  float* xmid = carry + kN * kRows;      // [kN][kRows]: state after the tile's first sub-tile
-  float* x0s = xmid + kN * kRows;        // [kN][kRows]: saved state at the tile start
-  float* a2s = x0s + kN * kRows;         // [kN][kRows]: A * log2(e)
+  f32x4* bcq = reinterpret_cast<f32x4*>(smem_f);   // [kP][kTB] B/C quads of the tile
+  // per-lane, per-pair scalars that persist across pairs / tiles live in LDS
+  // ([pair][lane] f32x2: conflict-free ds_read_b64), read and written once per
+  // pair and tile -- keeps the fully unrolled pair loop within 256 VGPRs
+  f32x2* carry_s = reinterpret_cast<f32x2*>(bcq + kBCQ);   // adjoint carried into the previous tile
+  f32x2* dA_s = carry_s + kP * kRows;                      // dA accumulators
+  f32x2* x0_s = dA_s + kP * kRows;                         // saved state at the tile start
+  f32x2* a2_s = x0_s + kP * kRows;                         // A * log2(e)
 
   const int lane = threadIdx.x;
   const int lin = xcd_remap(blockIdx.x, a.total_blocks);
@@ -163,8 +182,8 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   const int L_ = a.seqlen;
   const bool hasZ = a.z != nullptr;
   const bool softplus = a.softplus != 0;
-  const int my_d = dbase + lane;
   const bool my_ok = lane < nrows;
+  const int my_d = dbase + lane;
   const int my_dc = dbase + min(lane, nrows - 1);   // lanes past the group end mirror a valid row (never stored)
 
   const TI* __restrict__ urow = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs + (int64_t)my_dc * a.u_ds;
@@ -174,213 +193,209 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   TI* __restrict__ durow = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)my_dc * a.du_ds;
   TI* __restrict__ ddrow = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)my_dc * a.ddt_ds;
   TI* __restrict__ dzrow = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)my_dc * a.dz_ds;
-  const float* __restrict__ Arow = a.A + (int64_t)my_dc * a.dstate;
   const float* __restrict__ csrow = a.chunk_states + ((int64_t)b * a.dim + my_dc) * a.n_states * a.dstate;
+  const float* __restrict__ bcsrc = a.bct + (int64_t)bg * L_ * (2 * kN);
 
-  // per-lane, per-state scalars live in LDS ([n][lane]: conflict-free) so the
-  // n-loop never waits on global memory
 #pragma unroll
-  for (int n = 0; n < kN; ++n) {
-    carry[n * kRows + lane] = 0.f;
-    a2s[n * kRows + lane] = n < a.dstate ? Arow[n] * kLog2e : 0.f;
+  for (int p = 0; p < kP; ++p) {
+    const int n0 = 2 * p;
+    f32x2 av;
+    av.x = n0 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0] * kLog2e : 0.f;
+    av.y = n0 + 1 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0 + 1] * kLog2e : 0.f;
+    a2_s[p * kRows + lane] = av;
+    carry_s[p * kRows + lane] = f32x2{0.f, 0.f};
+    dA_s[p * kRows + lane] = f32x2{0.f, 0.f};
   }
-  // dA_n accumulators: a register ring rotated once per n step (the n-loop is
-  // not unrolled), so dAr[0] always belongs to the current n
-  float dAr[kN];
-#pragma unroll
-  for (int n = 0; n < kN; ++n) dAr[n] = 0.f;
   const float Dv = a.D ? a.D[my_dc] : 0.f;
   const float biasv = a.delta_bias ? a.delta_bias[my_dc] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
 
-  // raw vectors of one sub-tile -> per-position scalars
-  auto prep = [&](const uint4 (&rd)[kVPS], const uint4 (&ru)[kVPS], const uint4 (&rz)[kVPS],
-                  const uint4 (&rg)[kVPS], int p0, int t, float& dtv, float& sgv, float& uv, float& gyv, float& gzv) {
-    uv = elem_f<TI>(ru[t / VI], t % VI);
-    const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
-    const float go = elem_f<TI>(rg[t / VI], t % VI);
-    const bool live = p0 + t < L_;
-    const float d = softplus ? softplus_f(r) : r;
-    // d softplus/dr = sigmoid(r) (torch: gradient 1 above the threshold 20)
-    sgv = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
-    dtv = live ? d : 0.f;
-    if (hasZ) {
-      const float zv = elem_f<TI>(rz[t / VI], t % VI);
-      const float sgz = sigmoid_f(zv);
-      gyv = go * zv * sgz;                              // dout * silu(z)
-      gzv = go * sgz * (1.f + zv * (1.f - sgz));        // dout * silu'(z)
-    } else {
-      gyv = go;
-      gzv = 0.f;
-    }
-  };
-  auto load_raw = [&](int p0, bool full, uint4 (&ru)[kVPS], uint4 (&rd)[kVPS], uint4 (&rz)[kVPS],
-                      uint4 (&rg)[kVPS]) {
-    load_row_sub<TI>(urow, p0, L_, full, ru);
-    load_row_sub<TI>(drow, p0, L_, full, rd);
-    if (hasZ) {
-      load_row_sub<TI>(zrow, p0, L_, full, rz);
-    } else {
+  // ---- prefetch registers: one tile's rows, B/C quads and saved start state
+  uint4 ru[kVT], rd[kVT], rz[kVT], rg[kVT];
+  f32x4 pbc[kBCPer];
+  auto prefetch = [&](int ti) {
+    const int l0 = ti * kTB;
+    const bool full = kAligned && (l0 + kTB <= L_);
+    load_row_tile<TI>(urow, l0, L_, full, ru);
+    load_row_tile<TI>(drow, l0, L_, full, rd);
+    if (hasZ) load_row_tile<TI>(zrow, l0, L_, full, rz);
+    load_row_tile<TI>(grow, l0, L_, full, rg);
 #pragma unroll
-      for (int k = 0; k < kVPS; ++k) rz[k] = make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < kBCPer; ++k) {       // quad q = lane + 64 k -> (pair q / kTB, position q % kTB)
+      const int q = lane + k * kRows;
+      const int pp = q / kTB, t = q % kTB;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (q < kBCQ && l0 + t < L_) {
+        const float* row = bcsrc + (int64_t)(l0 + t) * (2 * kN);
+        const float2 bb = *reinterpret_cast<const float2*>(row + 2 * pp);
+        const float2 cc = *reinterpret_cast<const float2*>(row + kN + 2 * pp);
+        v = f32x4{bb.x, bb.y, cc.x, cc.y};
+      }
+      pbc[k] = v;
     }
-    load_row_sub<TI>(grow, p0, L_, full, rg);
   };
 
   const int ntiles = (L_ + kTB - 1) / kTB;
+  prefetch(ntiles - 1);
   for (int ti = ntiles - 1; ti >= 0; --ti) {
     const int l0 = ti * kTB;
-    const bool has_hi = l0 + kSub < L_;            // second sub-tile has live positions
-    __syncthreads();  // previous tile is done with bcT / xmid / x0s
-    // saved tile-start state -> LDS (zero for the first tile)
+    const bool full = kAligned && (l0 + kTB <= L_);
+    __syncthreads();                             // previous tile is done with the B/C quads
 #pragma unroll
-    for (int n = 0; n < kN; ++n) x0s[n * kRows + lane] = (ti > 0 && n < a.dstate) ? csrow[(ti - 1) * a.dstate + n] : 0.f;
-    {   // B/C tile, transposed to [2kN][kTB] (per-n rows of positions)
-      const float* src = a.bct + ((int64_t)bg * L_ + l0) * (2 * kN);
-      const int nval = min(kTB, L_ - l0) * (2 * kN);
-      for (int v = lane; v < kTB * 2 * kN; v += kRows) {
-        const int t = v / (2 * kN), jn = v % (2 * kN);
-        bcT[jn * kTB + t] = v < nval ? src[v] : 0.f;
+    for (int k = 0; k < kBCPer; ++k) {
+      const int q = lane + k * kRows;
+      if (q < kBCQ) bcq[q] = pbc[k];
+    }
+    // this tile's per-position scalars (from the prefetched raw rows)
+    float dt[kTB], dtu[kTB], gy[kTB];
+#pragma unroll
+    for (int t = 0; t < kTB; ++t) {
+      const float uv = elem_f<TI>(ru[t / VI], t % VI);
+      const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
+      const float go = elem_f<TI>(rg[t / VI], t % VI);
+      float d = softplus ? softplus_f(r) : r;
+      d = (l0 + t < L_) ? d : 0.f;
+      dt[t] = d;
+      dtu[t] = d * uv;
+      if (hasZ) {
+        const float zv = elem_f<TI>(rz[t / VI], t % VI);
+        gy[t] = go * zv * sigmoid_f(zv);          // dout * silu(z)
+      } else {
+        gy[t] = go;
       }
     }
-    __syncthreads();
-
-    // ---- state after the first sub-tile (restart point of the second), from the saved tile-start state
-    if (has_hi) {
-      float dt[kSub], dtu[kSub];
-      {
-        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
-        load_raw(l0, kAligned, ru, rd, rz, rg);   // l0 + kSub < L: the first sub-tile is full
+    // saved state at the tile start -> LDS (its latency overlaps the prep math and the barrier)
 #pragma unroll
-        for (int t = 0; t < kSub; ++t) {
-          float sgv, uv, gyv, gzv;
-          prep(rd, ru, rz, rg, l0, t, dt[t], sgv, uv, gyv, gzv);
-          dtu[t] = dt[t] * uv;
+    for (int p = 0; p < kP; ++p) {
+      f32x2 v = {0.f, 0.f};
+      if (ti > 0) {
+        const float* cs = csrow + (int64_t)(ti - 1) * a.dstate;
+        if ((a.dstate & 1) == 0) {
+          if (2 * p < a.dstate) v = *reinterpret_cast<const f32x2*>(cs + 2 * p);
+        } else {
+          if (2 * p < a.dstate) v.x = cs[2 * p];
+          if (2 * p + 1 < a.dstate) v.y = cs[2 * p + 1];
         }
       }
-#pragma unroll 1
-      for (int n = 0; n < kN; ++n) {
-        const float A2n = a2s[n * kRows + lane];
-        float x = x0s[n * kRows + lane];
-        const float* Bt = bcT + n * kTB;
+      x0_s[p * kRows + lane] = v;
+    }
+    __syncthreads();                             // B/C quads staged
+    if (ti > 0) prefetch(ti - 1);                // next tile's loads fly under this tile's math
+
+    f32x2 Y2[kTB], S2[kTB], Q2[kTB];
 #pragma unroll
-        for (int t = 0; t < kSub; ++t) x = fmaf(fast_exp2(dt[t] * A2n), x, dtu[t] * Bt[t]);
-        xmid[n * kRows + lane] = x;
+    for (int t = 0; t < kTB; ++t) { Y2[t] = f32x2{0.f, 0.f}; S2[t] = f32x2{0.f, 0.f}; Q2[t] = f32x2{0.f, 0.f}; }
+
+#pragma unroll 1
+    for (int p = 0; p < kP; ++p) {
+      const f32x2 A2p = a2_s[p * kRows + lane];
+      f32x4 bc[kTB];
+#pragma unroll
+      for (int t = 0; t < kTB; ++t) bc[t] = bcq[p * kTB + t];
+      // forward sweep: states and decays of this pair over the tile
+      f32x2 xs[kTB], as[kTB];
+      const f32x2 x0p = x0_s[p * kRows + lane];
+      f32x2 x = x0p;
+#pragma unroll
+      for (int t = 0; t < kTB; ++t) {
+        const f32x2 arg = A2p * dt[t];
+        const f32x2 aa = {fast_exp2(arg.x), fast_exp2(arg.y)};
+        x = aa * x + bc[t].lo * dtu[t];
+        xs[t] = x;
+        as[t] = aa;
+        Y2[t] = bc[t].hi * x + Y2[t];
+      }
+      // dC_t,n = sum over the wave's channels of gy_t x_t,n
+      {
+        float red[2 * kTB];
+#pragma unroll
+        for (int t = 0; t < kTB; ++t) {
+          const f32x2 v = my_ok ? xs[t] * gy[t] : f32x2{0.f, 0.f};
+          red[2 * t] = v.x;
+          red[2 * t + 1] = v.y;
+        }
+        const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+        const int j = lane / (64 / (2 * kTB));
+        const int t = j / 2, n = 2 * p + (j & 1);
+        if ((lane & (64 / (2 * kTB) - 1)) == 0 && n < a.dstate && l0 + t < L_)
+          a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 1) * L_ + l0 + t] = tot;
+      }
+      // reverse sweep: adjoint of the state
+      f32x2 h = carry_s[p * kRows + lane];
+      f32x2 dAp = dA_s[p * kRows + lane];
+      float red[2 * kTB];
+#pragma unroll
+      for (int t = kTB - 1; t >= 0; --t) {
+        h = bc[t].hi * gy[t] + h;                  // + C_t gy_t
+        S2[t] = h * bc[t].lo + S2[t];
+        const f32x2 vb = my_ok ? h * dtu[t] : f32x2{0.f, 0.f};
+        red[2 * t] = vb.x;
+        red[2 * t + 1] = vb.y;
+        const f32x2 ha = h * as[t];
+        const f32x2 hax = ha * (t > 0 ? xs[t - 1] : x0p);
+        Q2[t] = hax * A2p + Q2[t];
+        dAp = hax * dt[t] + dAp;
+        h = ha;
+      }
+      carry_s[p * kRows + lane] = h;
+      dA_s[p * kRows + lane] = dAp;
+      {
+        const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+        const int j = lane / (64 / (2 * kTB));
+        const int t = j / 2, n = 2 * p + (j & 1);
+        if ((lane & (64 / (2 * kTB) - 1)) == 0 && n < a.dstate && l0 + t < L_)
+          a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 0) * L_ + l0 + t] = tot;
       }
     }
 
-    // ---- the two sub-tiles, last first
-#pragma unroll 1
-    for (int sub = has_hi ? 1 : 0; sub >= 0; --sub) {
-      const int p0 = l0 + sub * kSub;
-      const bool full = kAligned && (p0 + kSub <= L_);
-      float dt[kSub], dtu[kSub], gy[kSub];
-      {
-        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
-        load_raw(p0, full, ru, rd, rz, rg);
+    // ---- per-position outputs of my channel (this tile's rows re-read: L2 hits)
+    uint4 cu[kVT], cd[kVT], cz[kVT], cg[kVT];
+    load_row_tile<TI>(urow, l0, L_, full, cu);
+    load_row_tile<TI>(drow, l0, L_, full, cd);
+    if (hasZ) load_row_tile<TI>(zrow, l0, L_, full, cz);
+    load_row_tile<TI>(grow, l0, L_, full, cg);
+    float o_du[kTB], o_dd[kTB], o_dz[kTB];
 #pragma unroll
-        for (int t = 0; t < kSub; ++t) {
-          float sgv, uv, gzv;
-          prep(rd, ru, rz, rg, p0, t, dt[t], sgv, uv, gy[t], gzv);
-          dtu[t] = dt[t] * uv;
-        }
+    for (int t = 0; t < kTB; ++t) {
+      const float uv = elem_f<TI>(cu[t / VI], t % VI);
+      const float r = elem_f<TI>(cd[t / VI], t % VI) + biasv;
+      const float go = elem_f<TI>(cg[t / VI], t % VI);
+      const float S = S2[t].x + S2[t].y;
+      const float Q = (Q2[t].x + Q2[t].y) * kLn2;   // A2 carries log2(e)
+      const float y = fmaf(Dv, uv, Y2[t].x + Y2[t].y);
+      const float sg = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
+      float gyv = go;
+      float gz = 0.f;
+      if (hasZ) {
+        const float zv = elem_f<TI>(cz[t / VI], t % VI);
+        const float sgz = sigmoid_f(zv);
+        gyv = go * zv * sgz;
+        gz = go * sgz * (1.f + zv * (1.f - sgz));
       }
-      // S_t = sum_n h B ;  Q_t = sum_n h A a x_{t-1} ;  ys_t = sum_n C x
-      float ys[kSub], S[kSub], Q[kSub];
-#pragma unroll
-      for (int t = 0; t < kSub; ++t) { ys[t] = 0.f; S[t] = 0.f; Q[t] = 0.f; }
-
-#pragma unroll 1
-      for (int n = 0; n < kN; ++n) {
-        const bool nok = n < a.dstate;
-        const float A2n = a2s[n * kRows + lane];
-        const float An = A2n * kLn2;
-        const float x0n = (sub ? xmid : x0s)[n * kRows + lane];
-        const float* Bt = bcT + n * kTB + sub * kSub;
-        const float* Ct = bcT + (kN + n) * kTB + sub * kSub;
-        // forward sweep: states and decays of this sub-tile
-        float xs[kSub], as[kSub];
-        float x = x0n;
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) {
-          const float aa = fast_exp2(dt[t] * A2n);
-          x = fmaf(aa, x, dtu[t] * Bt[t]);
-          xs[t] = x;
-          as[t] = aa;
-          ys[t] = fmaf(Ct[t], x, ys[t]);
-        }
-        float red[kSub];
-        // dC_t,n = sum over the wave's channels of gy_t x_t,n
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) red[t] = my_ok ? gy[t] * xs[t] : 0.f;
-        {
-          const float tot = wave_transpose_reduce<kSub>(red, lane);
-          const int t = lane / (64 / kSub);
-          if ((lane & (64 / kSub - 1)) == 0 && nok && p0 + t < L_)
-            a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 1) * L_ + p0 + t] = tot;
-        }
-        // reverse sweep
-        float h = carry[n * kRows + lane];
-        float dAn = 0.f;
-#pragma unroll
-        for (int t = kSub - 1; t >= 0; --t) {
-          h = fmaf(Ct[t], gy[t], h);
-          const float xp = t > 0 ? xs[t - 1] : x0n;
-          S[t] = fmaf(h, Bt[t], S[t]);
-          red[t] = my_ok ? h * dtu[t] : 0.f;              // dB_t,n contribution
-          const float ha = h * as[t];
-          const float hax = ha * xp;
-          Q[t] = fmaf(hax, An, Q[t]);
-          dAn = fmaf(hax, dt[t], dAn);
-          h = ha;
-        }
-        carry[n * kRows + lane] = h;
-        {
-          const float head = dAr[0] + dAn;
-#pragma unroll
-          for (int k = 0; k < kN - 1; ++k) dAr[k] = dAr[k + 1];
-          dAr[kN - 1] = head;
-        }
-        {
-          const float tot = wave_transpose_reduce<kSub>(red, lane);
-          const int t = lane / (64 / kSub);
-          if ((lane & (64 / kSub - 1)) == 0 && nok && p0 + t < L_)
-            a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 0) * L_ + p0 + t] = tot;
-        }
+      o_dz[t] = gz * y;
+      o_du[t] = fmaf(Dv, gyv, dt[t] * S);
+      const float dr = fmaf(uv, S, Q) * sg;
+      o_dd[t] = dr;
+      if (l0 + t < L_ && my_ok) {
+        dDacc = fmaf(gyv, uv, dDacc);
+        dbacc += dr;
       }
-
-      // ---- per-position outputs of my channel (raw vectors re-read: L1/L2 hits)
-      {
-        uint4 ru[kVPS], rd[kVPS], rz[kVPS], rg[kVPS];
-        load_raw(p0, full, ru, rd, rz, rg);
-        float o_du[kSub], o_dd[kSub], o_dz[kSub];
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) {
-          float dtv, sgv, uv, gyv, gzv;
-          prep(rd, ru, rz, rg, p0, t, dtv, sgv, uv, gyv, gzv);
-          const float y = fmaf(Dv, uv, ys[t]);
-          o_dz[t] = gzv * y;
-          o_du[t] = fmaf(Dv, gyv, dtv * S[t]);
-          const float dr = fmaf(uv, S[t], Q[t]) * sgv;
-          o_dd[t] = dr;
-          if (p0 + t < L_ && my_ok) {
-            dDacc = fmaf(gyv, uv, dDacc);
-            dbacc += dr;
-          }
-        }
-        if (my_ok) {
-          store_row_sub<TI>(durow, p0, L_, full, o_du);
-          store_row_sub<TI>(ddrow, p0, L_, full, o_dd);
-          if (hasZ) store_row_sub<TI>(dzrow, p0, L_, full, o_dz);
-        }
-      }
+    }
+    if (my_ok) {
+      store_row_tile<TI>(durow, l0, L_, full, o_du);
+      store_row_tile<TI>(ddrow, l0, L_, full, o_dd);
+      if (hasZ) store_row_tile<TI>(dzrow, l0, L_, full, o_dz);
     }
   }
 
   if (my_ok) {
     // slab_a is [b][n][d]: coalesced along d
 #pragma unroll
-    for (int n = 0; n < kN; ++n) a.slab_a[((int64_t)b * kN + n) * a.dim + my_d] = dAr[n];
+    for (int p = 0; p < kP; ++p) {
+      const f32x2 v = dA_s[p * kRows + lane];
+      a.slab_a[((int64_t)b * kN + 2 * p) * a.dim + my_d] = v.x;
+      a.slab_a[((int64_t)b * kN + 2 * p + 1) * a.dim + my_d] = v.y;
+    }
     a.slab_d[(int64_t)b * a.dim + my_d] = dDacc;
     a.slab_bias[(int64_t)b * a.dim + my_d] = dbacc;
   }
@@ -471,7 +486,7 @@ static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
 
 template <typename TI, int kN>
 static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
-  const size_t lds = (size_t)2 * kN * kTB * 4 + (size_t)4 * kN * kRows * 4;   // bcT + carry, xmid, x0s, a2s
+  const size_t lds = (size_t)(kN / 2) * kTB * 16 + (size_t)4 * (kN / 2) * kRows * 8;   // B/C quads + carry, dA, x0, A
   if (aligned)
     hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else

@@ -165,6 +165,18 @@ class PatchEmbed(nn.Module):
         return out.reshape(Bsz, -1, w.shape[0])
 
 
+def _gpu_sdpa_backends():
+    """Backend priority for the towers' attention on MI355X: the memory-efficient
+    kernel first (measured at C2, 197 tokens x 12 heads x 64: attention block
+    fwd+bwd 2.36 ms vs 2.51 ms for the default choice), then flash, then math."""
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+    order = [SDPBackend.EFFICIENT_ATTENTION, SDPBackend.FLASH_ATTENTION, SDPBackend.MATH]
+    try:
+        return sdpa_kernel(order, set_priority=True)
+    except TypeError:  # older torch: no priority argument
+        return sdpa_kernel(order)
+
+
 class Attention(nn.Module):
     def __init__(self, dim, heads):
         super().__init__()
@@ -174,8 +186,16 @@ class Attention(nn.Module):
 
     def forward(self, x):
         Bsz, N, C = x.shape
-        qkv = self.qkv(x).reshape(Bsz, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
-        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+        # unbind (not index) the q/k/v slices: its backward stacks the three
+        # gradients in one write instead of zero-filling and accumulating a
+        # (3, B, H, N, D) buffer three times and copying it contiguous again
+        q, k, v = self.qkv(x).view(Bsz, N, 3, self.heads, C // self.heads).unbind(2)
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        if x.is_cuda:
+            with _gpu_sdpa_backends():
+                o = F.scaled_dot_product_attention(q, k, v)
+        else:
+            o = F.scaled_dot_product_attention(q, k, v)
         return self.proj(o.transpose(1, 2).reshape(Bsz, N, C))
 
 
