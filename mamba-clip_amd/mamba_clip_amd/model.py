@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import add_layernorm, add_rmsnorm, causal_conv1d, patch_im2col
+from .ops import add_layernorm, add_rmsnorm, causal_conv1d, linear_sk, patch_im2col, wleft_mm
 from .selective_scan_interface import selective_scan_fn
 
 
@@ -75,21 +75,22 @@ class MambaMixer(nn.Module):
         dt_in = hidden.dtype
         di, R, N = self.d_inner, self.dt_rank, self.d_state
         H = hidden.reshape(Bsz * L, dm)
-        xz = torch.mm(self.in_proj.weight.to(dt_in), H.t())                  # (2*di, B*L)
+        # projections: weight-left GEMMs with split-K weight gradients (ops.wleft_mm / linear_sk)
+        xz = wleft_mm(self.in_proj.weight, H.t())                             # (2*di, B*L)
         x, z = xz.split(di, dim=0)
         x = x.view(di, Bsz, L).transpose(0, 1)                                # (B, di, L) channel-major
         z = z.view(di, Bsz, L).transpose(0, 1)
         x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True)
-        x_dbl = torch.mm(self.x_proj.weight.to(dt_in), x.transpose(0, 1).reshape(di, Bsz * L))   # (R+2N, B*L)
+        x_dbl = wleft_mm(self.x_proj.weight, x.transpose(0, 1).reshape(di, Bsz * L))   # (R+2N, B*L)
         dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
-        delta = torch.mm(self.dt_proj.weight.to(dt_in), dt_raw).view(di, Bsz, L).transpose(0, 1)
+        delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
         Bm = Bm.view(N, Bsz, L).transpose(0, 1)                               # (B, N, L)
         Cm = Cm.view(N, Bsz, L).transpose(0, 1)
         A = -torch.exp(self.A_log.float())
         y = selective_scan_fn(x, delta, A, Bm, Cm, self.D.float(), z=z,
                               delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
         y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
-        out = torch.mm(y2.t(), self.out_proj.weight.to(dt_in).t())             # (B*L, d_model)
+        out = linear_sk(y2.t(), self.out_proj.weight)                          # (B*L, d_model)
         return out.view(Bsz, L, dm)
 
 
@@ -189,14 +190,14 @@ class Attention(nn.Module):
         # unbind (not index) the q/k/v slices: its backward stacks the three
         # gradients in one write instead of zero-filling and accumulating a
         # (3, B, H, N, D) buffer three times and copying it contiguous again
-        q, k, v = self.qkv(x).view(Bsz, N, 3, self.heads, C // self.heads).unbind(2)
+        q, k, v = linear_sk(x, self.qkv.weight, self.qkv.bias).view(Bsz, N, 3, self.heads, C // self.heads).unbind(2)
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         if x.is_cuda:
             with _gpu_sdpa_backends():
                 o = F.scaled_dot_product_attention(q, k, v)
         else:
             o = F.scaled_dot_product_attention(q, k, v)
-        return self.proj(o.transpose(1, 2).reshape(Bsz, N, C))
+        return linear_sk(o.transpose(1, 2).reshape(Bsz, N, C), self.proj.weight, self.proj.bias)
 
 
 class ViTBlock(nn.Module):
@@ -221,7 +222,7 @@ class ViTBlock(nn.Module):
         y, h = add_layernorm(m, h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         a = self.attn(y)
         y, h = add_layernorm(a, h, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        return self.fc2(F.gelu(self.fc1(y))), h
+        return linear_sk(F.gelu(linear_sk(y, self.fc1.weight, self.fc1.bias)), self.fc2.weight, self.fc2.bias), h
 
 
 class VisionTransformer(nn.Module):

@@ -304,3 +304,106 @@ def patch_im2col(img, patch):
     _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(img.dtype), img.data_ptr(), out.data_ptr(),
                                    _lib.stream_handle(img.device)), "mc_patch_im2col")
     return out
+
+
+# ---------------------------------------------------------------------------- projections with split-K weight grads
+# The towers' weight gradients are GEMMs with a short output (N x K <= 3072 x
+# 3072) and a very long reduction (M = batch * tokens = 50432 at C2): one
+# library GEMM tiles the output into too few workgroups for 256 CUs (measured
+# on MI355X, tools/gemm_wgrad_ab.py: 231-610 TF/s).  Splitting M into s slabs
+# and summing the fp32 partials (one strided-batched GEMM + one reduction)
+# runs 1.3-1.8x faster and keeps the sum in fp32.
+def _split_factor(M, N, K):
+    s = 4 if N * K >= 2_000_000 else 8
+    while s > 1 and M % s:
+        s //= 2
+    return s
+
+
+def wgrad(G, X):
+    """G @ X in fp32 for G (N, M), X (M, K), any strides, M the long reduction dim."""
+    N, M = G.shape
+    K = X.shape[1]
+    s = _split_factor(M, N, K) if (G.is_cuda and M >= 8192) else 1
+    if s == 1:
+        return torch.mm(G, X).float()
+    Gs = G.unflatten(1, (s, M // s)).transpose(0, 1)        # (s, N, M/s)
+    Xs = X.unflatten(0, (s, M // s))                        # (s, M/s, K)
+    return torch.bmm(Gs, Xs, out_dtype=torch.float32).sum(0)
+
+
+def _compute_dtype(t):
+    if t.is_cuda and torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return t.dtype
+
+
+class LinearSK(torch.autograd.Function):
+    """y = x @ w^T (+ b), autocast-aware; backward: dx = g @ w, dw = split-K g^T x (fp32), db = sum g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        dt = _compute_dtype(x)
+        xc, wc = x.to(dt), weight.to(dt)
+        bc = bias.to(dt) if bias is not None else None
+        with torch.autocast("cuda", enabled=False):
+            y = torch.nn.functional.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wc = ctx.saved_tensors
+        K = xc.shape[-1]
+        g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype)
+        x2 = xc.reshape(-1, K)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if xc.dim() == 2 and xc.stride(0) == 1 and xc.stride(1) != 1:
+                # x is a transposed (column-major) view, e.g. the mixer's channel-major
+                # scan output: produce dx in the same layout so the producer's
+                # backward needs no transpose copy
+                dx = torch.mm(wc.t(), g2.t()).t()
+            else:
+                dx = torch.mm(g2, wc).view(xc.shape)
+        if ctx.needs_input_grad[1]:
+            dw = wgrad(g2.t(), x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.sum(g2, 0, dtype=torch.float32)
+        return dx, dw, db
+
+
+def linear_sk(x, weight, bias=None):
+    return LinearSK.apply(x, weight, bias)
+
+
+class WeightLeftMM(torch.autograd.Function):
+    """y = w @ X for a weight w (N, K) and activations X (K, M) (channel-major GEMMs of the Mamba mixer)."""
+
+    @staticmethod
+    def forward(ctx, weight, X):
+        dt = _compute_dtype(X)
+        wc, Xc = weight.to(dt), X.to(dt)
+        with torch.autocast("cuda", enabled=False):
+            y = torch.mm(wc, Xc)
+        ctx.save_for_backward(wc, Xc)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        wc, Xc = ctx.saved_tensors
+        g = gy.to(wc.dtype)
+        dw = dX = None
+        if ctx.needs_input_grad[0]:
+            dw = wgrad(g, Xc.t())
+        if ctx.needs_input_grad[1]:
+            if Xc.stride(0) == 1 and Xc.stride(1) != 1:
+                dX = torch.mm(g.t(), wc).t()      # X is a transposed view: keep its layout (no copy downstream)
+            else:
+                dX = torch.mm(wc.t(), g)
+        return dw, dX
+
+
+def wleft_mm(weight, X):
+    return WeightLeftMM.apply(weight, X)

@@ -84,3 +84,20 @@ def test_schedulers_match_reference_formulas():
     assert g(1) == 1.0 and g(50) == 2.0
     h = const_lr_cooldown(o, 1.0, 0, 100, 20, cooldown_power=1.0, cooldown_end_lr=0.0)
     assert h(79) == 1.0 and abs(h(90) - 0.5) < 1e-12 and o.param_groups[0]["lr"] == h(90)
+
+
+def test_split_k_projection_autograd_cpu():
+    """linear_sk / wleft_mm (split-K weight-gradient projections) against autograd, incl. transposed-view inputs."""
+    import torch
+    from mamba_clip_amd.ops import linear_sk, wleft_mm
+    torch.manual_seed(0)
+    x = torch.randn(64, 16, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(8, 16, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(8, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda x, w, b: linear_sk(x, w, b), (x, w, b))
+    xt = torch.randn(16, 64, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda xt, w: linear_sk(xt.t(), w, None), (xt, w))
+    X = torch.randn(16, 64, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda w, X: wleft_mm(w, X), (w, X))
+    H = torch.randn(64, 16, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda w, H: wleft_mm(w, H.t()), (w, H))

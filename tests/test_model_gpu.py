@@ -277,3 +277,23 @@ def test_cli_synthetic_tiny(stage, capsys):
     line = [l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["pairs_per_sec"] > 0 and out["final"]["loss"] is not None
+
+
+def test_split_k_weight_grad_matches_fp32():
+    """wgrad (strided-batched split-K, fp32 partial sums) vs an fp64 product, at a C2 tower shape."""
+    import torch
+    from mamba_clip_amd.ops import wgrad
+    torch.manual_seed(0)
+    M, N, K = 50432, 768, 768
+    g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    got = wgrad(g.t(), x)
+    ref = (g.double().t() @ x.double()).float()
+    assert got.dtype == torch.float32
+    rel = float((got - ref).abs().max() / ref.abs().max())
+    assert rel < 1e-4, rel          # fp32 accumulation of exact bf16 products
+    # channel-major operand (the mixer's in_proj: X = H^T view)
+    X = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
+    got2 = wgrad(g.t(), X.t())
+    ref2 = (g.double().t() @ X.double().t()).float()
+    assert float((got2 - ref2).abs().max() / ref2.abs().max()) < 1e-4
