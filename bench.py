@@ -104,10 +104,23 @@ def scan_roofline(iters, warmup=3):
     achieved = nbytes / (ms * 1e-3) / 1e9
     del u, z, delta, Bm, Cm
     torch.cuda.empty_cache()
+    traffic, traffic_src = _pmc_traffic()
     return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
+            "traffic_source": traffic_src, "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of the same kernel at the same config, from the committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh; calibration in the JSON).  PMC counters
+    cannot be read from inside a timed run, so the newest committed measurement is reported."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "scan_fwd_c4_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return (int(d["hbm_bytes"]) if d.get("hbm_bytes") else None), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(args, model_name):

@@ -1,0 +1,63 @@
+"""Per-launch HBM bytes of the roofline kernel from the FETCH_SIZE / WRITE_SIZE passes (see pmc_traffic.py).
+
+Writes <outdir>/scan_fwd_c4_traffic.json; copy it to profiles/<round>/ for bench.py.
+"""
+import csv
+import glob
+import json
+import statistics
+import sys
+
+out = sys.argv[1]
+
+
+def per_dispatch(pattern, counter):
+    vals = {}
+    for f in glob.glob(f"{out}/{pattern}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            key = (r["Kernel_Name"], r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    return vals
+
+
+def pick(vals, sub):
+    v = [x for (k, _), x in vals.items() if sub(k)]
+    return statistics.median(v) if v else None
+
+
+fetch = per_dispatch("fetch", "FETCH_SIZE")
+write = per_dispatch("write", "WRITE_SIZE")
+is_copy = lambda k: "copyBuffer" in k  # noqa: E731  (the runtime blit behind clone())
+is_scan = lambda k: "scan_fwd" in k  # noqa: E731
+is_relayout = lambda k: "bc_relayout" in k  # noqa: E731
+calib_bytes = (1 << 30) * 2                        # 2 GiB read (and written) per clone
+f_copy, w_copy = pick(fetch, is_copy), pick(write, is_copy)
+read_scale = calib_bytes / (f_copy * 1024) if f_copy else None
+write_scale = calib_bytes / (w_copy * 1024) if w_copy else None
+# the scan's own load pattern (16 B per lane, four lanes per 64-B row chunk)
+# reads differently through the counters: calibrated by tools/ubench/fetch_calib
+fcal = per_dispatch("fcal", "FETCH_SIZE")
+f_pat = pick(fcal, lambda k: True)
+pat_bytes = 64 * 3072 * 4096 * 2
+pat_scale = pat_bytes / (f_pat * 1024) if f_pat else read_scale
+f_scan, w_scan = pick(fetch, is_scan), pick(write, is_scan)
+f_rel, w_rel = pick(fetch, is_relayout) or 0.0, pick(write, is_relayout) or 0.0
+alg = 64 * 3072 * 4096 * 8 + 2 * 64 * 16 * 4096 * 2 + (3072 * 16 + 2 * 3072) * 4
+res = {
+    "kernel": "selective_scan_fwd @ C4 (bc_relayout + scan kernel), per launch",
+    "counters": "FETCH_SIZE, WRITE_SIZE (KB), separate rocprofv3 --pmc passes",
+    "calibration": {"stream": "bf16 clone of 2 GiB (runtime copyBuffer)", "fetch_kb": f_copy, "write_kb": w_copy,
+                    "read_scale": read_scale, "write_scale": write_scale,
+                    "scan_pattern": "tools/ubench/fetch_calib (1.5 GiB, the scan's staging pattern)",
+                    "scan_pattern_fetch_kb": f_pat, "scan_pattern_read_scale": pat_scale},
+    "scan_fetch_kb": f_scan, "scan_write_kb": w_scan, "relayout_fetch_kb": f_rel, "relayout_write_kb": w_rel,
+    "algorithmic_bytes": alg,
+}
+if f_scan is not None and read_scale and write_scale:
+    res["hbm_bytes"] = (f_scan * 1024 * pat_scale + f_rel * 1024 * read_scale
+                        + (w_scan + w_rel) * 1024 * write_scale)
+    res["hbm_over_algorithmic"] = res["hbm_bytes"] / alg
+json.dump(res, open(f"{out}/scan_fwd_c4_traffic.json", "w"), indent=1)
+print(json.dumps(res, indent=1))
