@@ -38,12 +38,13 @@ def test_library_loads_and_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mamba_clip_amd import _lib
     lib = _lib.load()
+    C = _lib.MC_SCAN_CHUNK          # saved-state granularity (8 positions)
     assert lib.mc_scan_n_chunks(0) == 0
     assert lib.mc_scan_n_chunks(1) == 1
-    assert lib.mc_scan_n_chunks(16) == 1
-    assert lib.mc_scan_n_chunks(17) == 2
-    assert lib.mc_scan_n_chunks(4096) == 256
-    assert lib.mc_scan_chunk_states_bytes(2, 3, 77, 16) == 2 * 3 * 5 * 16 * 4
+    assert lib.mc_scan_n_chunks(C) == 1
+    assert lib.mc_scan_n_chunks(C + 1) == 2
+    assert lib.mc_scan_n_chunks(4096) == 4096 // C
+    assert lib.mc_scan_chunk_states_bytes(2, 3, 77, 16) == 2 * 3 * ((77 + C - 1) // C) * 16 * 4
 
 
 def test_validation_errors_without_launch():
