@@ -80,6 +80,11 @@ typedef struct mc_scan_fwd_params {
   float* last_state;        /* nullable: (batch, dim, dstate) fp32 */
   void* workspace;          /* >= mc_scan_fwd_workspace_bytes(...) bytes, 16-B aligned */
   size_t workspace_bytes;
+  /* nullable; used only when z is given: the pre-gate output y + D u (itype,
+   * seqlen stride 1) -- the `out` upstream's forward returns next to out_z and
+   * its backward takes for dz.  A training caller passes it on to mc_scan_bwd. */
+  void* out_y;
+  int64_t out_y_batch_stride, out_y_dim_stride;
 } mc_scan_fwd_params;
 
 typedef struct mc_scan_bwd_params {
@@ -121,6 +126,10 @@ typedef struct mc_scan_bwd_params {
   float* ddelta_bias;
   void* workspace;            /* >= mc_scan_bwd_workspace_bytes(...) bytes, 256-B aligned */
   size_t workspace_bytes;
+  /* REQUIRED when z is given: the forward's pre-gate output (mc_scan_fwd_params.out_y),
+   * as upstream's bwd takes `out` for dz = dout * out * silu'(z) */
+  const void* out_y;
+  int64_t out_y_batch_stride, out_y_dim_stride;
 } mc_scan_bwd_params;
 
 /* number of MC_SCAN_CHUNK-long chunks covering seqlen */

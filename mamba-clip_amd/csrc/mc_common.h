@@ -110,6 +110,35 @@ __device__ __forceinline__ void st16_masked(T* __restrict__ p, const uint4& q, i
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void st16(void* p, const uint4& q) { *reinterpret_cast<uint4*>(p) = q; }
 
+// ---------------------------------------------------------------- raw buffer access
+// A buffer resource (V#) holds a wave-uniform base and byte range in SGPRs, so
+// a lane's address is ONE 32-bit VGPR offset instead of a 64-bit pointer, and
+// a read at or past num_records returns 0 instead of faulting: ragged tails are
+// loaded branch-free and masked where used.  Word 3 = raw 32-bit access, gfx9.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off, 0, 0);
+}
+// elements [0, nvalid) of a 16-B vector (nvalid wave-uniform)
+template <typename T>
+__device__ __forceinline__ void buf_st16_masked(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& q, int nvalid) {
+  constexpr int N = ElemTraits<T>::kVec;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i < nvalid) {
+      if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(word_of(q, i), r, off + 4 * i, 0, 0);
+      else __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(word_of(q, i >> 1) >> (16 * (i & 1))), r,
+                                                 off + 2 * i, 0, 0);
+    }
+  }
+}
+
 // exp2 on the transcendental unit (v_exp_f32)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }

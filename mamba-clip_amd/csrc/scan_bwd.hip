@@ -32,6 +32,7 @@
 //    small second kernel sums the slabs over waves / batches: deterministic,
 //    no atomics.
 #include <cstdlib>
+#include <type_traits>
 
 #include "scan_common.h"
 
@@ -48,10 +49,11 @@ struct BwdArgs {
   const float* A; const float* bct; const float* D; const float* delta_bias;
   const float* chunk_states;
   void* du; void* ddelta; void* dz;
-  float* slab_bc;                    // [b*G+g][nblk][kN][2][seqlen]
+  float* slab_bc;                    // [b*G+g][nblk][seqlen][2][kN]  (dB partials, then dC partials)
   float* slab_a;                     // [b][kN][dim] (dA partials, one owner per element)
   float* slab_d;                     // [b][dim]
   float* slab_bias;                  // [b][dim]
+  const void* y; int64_t y_bs, y_ds;  // forward's pre-gate output (required with z)
 };
 
 __device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
@@ -116,21 +118,25 @@ __device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane)
 
 // Own-row vector I/O: a lane reads / writes the kTB consecutive positions of
 // its own (b, d) row as 16-B vectors (no LDS staging of the rows: a wave
-// revisits its rows tile after tile, so L2 sees whole lines).
+// revisits its rows tile after tile, so L2 sees whole lines).  Addresses are a
+// wave-uniform base (SGPRs) + a 32-bit per-lane element offset, so each row
+// costs one VGPR instead of a 64-bit pointer pair (the host checks the range).
 template <typename TI>
-__device__ __forceinline__ void load_row_tile(const TI* __restrict__ p, int l0, int L, bool full,
+__device__ __forceinline__ void load_row_tile(const TI* __restrict__ base, uint32_t off, int l0, int L, bool full,
                                               uint4 (&q)[kTB / ElemTraits<TI>::kVec]) {
   constexpr int VI = ElemTraits<TI>::kVec;
 #pragma unroll
   for (int k = 0; k < kTB / VI; ++k) {
     const int col0 = l0 + k * VI;
-    if (full) q[k] = ld16(p + col0);
-    else q[k] = ld16_masked(p + col0, max(0, min(VI, L - col0)));
+    const TI* p = base + (uint32_t)(off + col0);
+    if (full) q[k] = ld16(p);
+    else q[k] = ld16_masked(p, max(0, min(VI, L - col0)));
   }
 }
 
 template <typename TI>
-__device__ __forceinline__ void store_row_tile(TI* __restrict__ p, int l0, int L, bool full, const float (&v)[kTB]) {
+__device__ __forceinline__ void store_row_tile(TI* __restrict__ base, uint32_t off, int l0, int L, bool full,
+                                               const float (&v)[kTB]) {
   constexpr int VI = ElemTraits<TI>::kVec;
 #pragma unroll
   for (int k = 0; k < kTB / VI; ++k) {
@@ -138,8 +144,9 @@ __device__ __forceinline__ void store_row_tile(TI* __restrict__ p, int l0, int L
 #pragma unroll
     for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
     const int col0 = l0 + k * VI;
-    if (full) st16(p + col0, pack_f<TI>(w));
-    else st16_masked(p + col0, pack_f<TI>(w), max(0, min(VI, L - col0)));
+    TI* p = base + (uint32_t)(off + col0);
+    if (full) st16(p, pack_f<TI>(w));
+    else st16_masked(p, pack_f<TI>(w), max(0, min(VI, L - col0)));
   }
 }
 
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   f32x2* dA_s = carry_s + kP * kRows;                      // dA accumulators
   f32x2* x0_s = dA_s + kP * kRows;                         // saved state at the tile start
   f32x2* a2_s = x0_s + kP * kRows;                         // A * log2(e)
+  float* dbc_s = reinterpret_cast<float*>(a2_s + kP * kRows);   // [kTB][2][kN] this tile's dB / dC sums
 
   const int lane = threadIdx.x;
   const int lin = xcd_remap(blockIdx.x, a.total_blocks);
@@ -186,23 +194,106 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   const int my_d = dbase + lane;
   const int my_dc = dbase + min(lane, nrows - 1);   // lanes past the group end mirror a valid row (never stored)
 
-  const TI* __restrict__ urow = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs + (int64_t)my_dc * a.u_ds;
-  const TI* __restrict__ drow = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs + (int64_t)my_dc * a.dt_ds;
-  const TI* __restrict__ zrow = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs + (int64_t)my_dc * a.z_ds;
-  const TI* __restrict__ grow = reinterpret_cast<const TI*>(a.dout) + (int64_t)b * a.go_bs + (int64_t)my_dc * a.go_ds;
-  TI* __restrict__ durow = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)my_dc * a.du_ds;
-  TI* __restrict__ ddrow = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)my_dc * a.ddt_ds;
-  TI* __restrict__ dzrow = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)my_dc * a.dz_ds;
-  const float* __restrict__ csrow = a.chunk_states + ((int64_t)b * a.dim + my_dc) * a.n_states * a.dstate;
+  // Row-block addressing.  kAligned: buffer resources (base + byte range of
+  // this wave's rows in SGPRs) and ONE 32-bit VGPR offset per access, rebuilt
+  // from an opaque lane id where used instead of being held across the pair
+  // loop; reads past a row block return 0, so ragged tails load branch-free
+  // and are masked where used.  !kAligned (odd strides): plain pointers.
+  const int64_t rows_u = (int64_t)b * a.u_bs + (int64_t)dbase * a.u_ds;
+  const int64_t rows_d = (int64_t)b * a.dt_bs + (int64_t)dbase * a.dt_ds;
+  const int64_t rows_z = hasZ ? (int64_t)b * a.z_bs + (int64_t)dbase * a.z_ds : rows_u;
+  const int64_t rows_g = (int64_t)b * a.go_bs + (int64_t)dbase * a.go_ds;
+  const TI* __restrict__ ub = reinterpret_cast<const TI*>(a.u) + rows_u;
+  const TI* __restrict__ db = reinterpret_cast<const TI*>(a.delta) + rows_d;
+  const TI* __restrict__ zb = hasZ ? reinterpret_cast<const TI*>(a.z) + rows_z : ub;
+  const TI* __restrict__ gb = reinterpret_cast<const TI*>(a.dout) + rows_g;
+  TI* __restrict__ dub = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)dbase * a.du_ds;
+  TI* __restrict__ ddb = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)dbase * a.ddt_ds;
+  TI* __restrict__ dzb = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)dbase * a.dz_ds;
+  const int64_t zds64 = hasZ ? a.z_ds : a.u_ds;
+  const TI* __restrict__ yb = hasZ ? reinterpret_cast<const TI*>(a.y) + (int64_t)b * a.y_bs + (int64_t)dbase * a.y_ds : ub;
+  const int64_t yds64 = hasZ ? a.y_ds : a.u_ds;
+  const float* __restrict__ csb = a.chunk_states + ((int64_t)b * a.dim + dbase) * a.n_states * a.dstate;
+  const uint32_t cs_ds = (uint32_t)(a.n_states * a.dstate);
   const float* __restrict__ bcsrc = a.bct + (int64_t)bg * L_ * (2 * kN);
+  auto row_of_lane = [&]() -> uint32_t { return (uint32_t)min(opaque_lane_id(), nrows - 1); };
+  auto span = [&](int64_t ds) -> uint32_t { return (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)); };
+  const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(ub, span(a.u_ds)), rs_d = make_rsrc(db, span(a.dt_ds));
+  const __amdgpu_buffer_rsrc_t rs_z = make_rsrc(zb, span(zds64)), rs_g = make_rsrc(gb, span(a.go_ds));
+  const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(yb, span(yds64));
+  const __amdgpu_buffer_rsrc_t rs_du = make_rsrc(dub, span(a.du_ds)), rs_dd = make_rsrc(ddb, span(a.ddt_ds));
+  const __amdgpu_buffer_rsrc_t rs_dz = make_rsrc(hasZ ? (const void*)dzb : (const void*)dub, span(hasZ ? a.dz_ds : a.du_ds));
+  const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(csb, (uint32_t)nrows * cs_ds * 4u);
+  const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(bcsrc, (uint32_t)L_ * (2 * kN) * 4u);
+  const __amdgpu_buffer_rsrc_t rs_slab =
+      make_rsrc(a.slab_bc + ((int64_t)bg * a.nblk + dblk) * L_ * (2 * kN), (uint32_t)L_ * (2 * kN) * 4u);
+  // one row tile of a tensor: [l0, l0 + kTB) of this lane's row
+  auto tile_in = [&](const __amdgpu_buffer_rsrc_t& rs, const TI* base, int64_t ds, int l0, bool full,
+                     uint4 (&q)[kVT]) {
+    const uint32_t rl = row_of_lane();
+    if constexpr (kAligned) {
+#pragma unroll
+      for (int k = 0; k < kVT; ++k)
+        q[k] = buf_ld16(rs, (rl * (uint32_t)ds + (uint32_t)(l0 + k * VI)) * (uint32_t)sizeof(TI));
+    } else {
+      load_row_tile<TI>(base + (int64_t)rl * ds, 0, l0, L_, full, q);
+    }
+  };
+  auto pack_tile = [&](const float (&v)[kTB], uint4 (&q)[kVT]) {
+#pragma unroll
+    for (int k = 0; k < kVT; ++k) {
+      float w[VI];
+#pragma unroll
+      for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
+      q[k] = pack_f<TI>(w);
+    }
+  };
+  // kAligned only: store a packed row tile (positions past L masked off)
+  auto tile_out_q = [&](const __amdgpu_buffer_rsrc_t& rs, int64_t ds, uint32_t rl, int l0, bool full,
+                        const uint4 (&q)[kVT]) {
+#pragma unroll
+    for (int k = 0; k < kVT; ++k) {
+      const uint32_t off = (rl * (uint32_t)ds + (uint32_t)(l0 + k * VI)) * (uint32_t)sizeof(TI);
+      if (full) buf_st16(rs, off, q[k]);
+      else buf_st16_masked<TI>(rs, off, q[k], max(0, min(VI, L_ - (l0 + k * VI))));
+    }
+  };
+  auto tile_out = [&](const __amdgpu_buffer_rsrc_t& rs, TI* base, int64_t ds, uint32_t rl, int l0, bool full,
+                      const float (&v)[kTB]) {
+    if constexpr (kAligned) {
+      uint4 q[kVT];
+      pack_tile(v, q);
+      tile_out_q(rs, ds, rl, l0, full, q);
+    } else {
+      store_row_tile<TI>(base + (int64_t)rl * ds, 0, l0, L_, full, v);
+    }
+  };
 
+  // exact-width state rows (dstate == kN, the common case): A and the saved
+  // states move as 16-B vectors, issued back to back with one wait
+  const bool vecN = a.dstate == kN;
+  if (vecN) {
+    const f32x4* A4 = reinterpret_cast<const f32x4*>(a.A + (int64_t)my_dc * kN);
+    f32x4 av[kN / 4];
+#pragma unroll
+    for (int q = 0; q < kN / 4; ++q) av[q] = A4[q] * kLog2e;
+#pragma unroll
+    for (int q = 0; q < kN / 4; ++q) {
+      a2_s[(2 * q) * kRows + lane] = av[q].lo;
+      a2_s[(2 * q + 1) * kRows + lane] = av[q].hi;
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      const int n0 = 2 * p;
+      f32x2 av;
+      av.x = n0 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0] * kLog2e : 0.f;
+      av.y = n0 + 1 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0 + 1] * kLog2e : 0.f;
+      a2_s[p * kRows + lane] = av;
+    }
+  }
 #pragma unroll
   for (int p = 0; p < kP; ++p) {
-    const int n0 = 2 * p;
-    f32x2 av;
-    av.x = n0 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0] * kLog2e : 0.f;
-    av.y = n0 + 1 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0 + 1] * kLog2e : 0.f;
-    a2_s[p * kRows + lane] = av;
     carry_s[p * kRows + lane] = f32x2{0.f, 0.f};
     dA_s[p * kRows + lane] = f32x2{0.f, 0.f};
   }
@@ -210,82 +301,126 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   const float biasv = a.delta_bias ? a.delta_bias[my_dc] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
 
-  // ---- prefetch registers: one tile's rows, B/C quads and saved start state
+  // ---- prefetch registers: one tile's rows, B/C quads and saved start
+  // state.  Tiles are walked last to first, so only the first tile visited can
+  // be ragged: every prefetch inside the loop is a full tile and (kAligned)
+  // compiles to unconditional 16-B loads -- no control flow around the loads,
+  // so nothing forces a vmcnt wait before the loads are consumed a tile later.
   uint4 ru[kVT], rd[kVT], rz[kVT], rg[kVT];
+  // 16-bit inputs: rows are fetched for TWO tiles at a time (the loads of
+  // both go out back to back, so each 128-B line a lane touches is fetched
+  // once for 16 positions instead of once per 8); the second tile waits here
+  constexpr bool kPairs = kAligned && sizeof(TI) == 2;
+  uint4 su[kVT], sd[kVT], sz[kVT], sg[kVT];
   f32x4 pbc[kBCPer];
-  auto prefetch = [&](int ti) {
+  f32x4 px0[kN / 4];
+  auto load_rows = [&](int ti, bool full, uint4 (&qu)[kVT], uint4 (&qd)[kVT], uint4 (&qz)[kVT], uint4 (&qg)[kVT]) {
     const int l0 = ti * kTB;
-    const bool full = kAligned && (l0 + kTB <= L_);
-    load_row_tile<TI>(urow, l0, L_, full, ru);
-    load_row_tile<TI>(drow, l0, L_, full, rd);
-    if (hasZ) load_row_tile<TI>(zrow, l0, L_, full, rz);
-    load_row_tile<TI>(grow, l0, L_, full, rg);
+    tile_in(rs_u, ub, a.u_ds, l0, full, qu);
+    tile_in(rs_d, db, a.dt_ds, l0, full, qd);
+    tile_in(rs_z, zb, zds64, l0, full, qz);     // (no z: a harmless re-read of u, no branch)
+    tile_in(rs_g, gb, a.go_ds, l0, full, qg);
+  };
+  auto prefetch_bc = [&](int ti) {
+    const int l0 = ti * kTB;
 #pragma unroll
     for (int k = 0; k < kBCPer; ++k) {       // quad q = lane + 64 k -> (pair q / kTB, position q % kTB)
       const int q = lane + k * kRows;
-      const int pp = q / kTB, t = q % kTB;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (q < kBCQ && l0 + t < L_) {
-        const float* row = bcsrc + (int64_t)(l0 + t) * (2 * kN);
-        const float2 bb = *reinterpret_cast<const float2*>(row + 2 * pp);
-        const float2 cc = *reinterpret_cast<const float2*>(row + kN + 2 * pp);
-        v = f32x4{bb.x, bb.y, cc.x, cc.y};
-      }
-      pbc[k] = v;
+      const int pp = min(q / kTB, kP - 1), t = q % kTB;
+      // positions past L read as 0 (buffer range); quads q >= kBCQ are never stored
+      const uint32_t off = (uint32_t)(((l0 + t) * (2 * kN) + 2 * pp) * 4);
+      const uint2 bb = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_bc, off, 0, 0));
+      const uint2 cc = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_bc, off + kN * 4, 0, 0));
+      pbc[k] = f32x4{__uint_as_float(bb.x), __uint_as_float(bb.y), __uint_as_float(cc.x), __uint_as_float(cc.y)};
     }
   };
+  // saved state at the start of tile ti (zero for ti == 0): the row's first
+  // kN floats as kN/4 16-B loads (dword-aligned for any dstate; entries past
+  // dstate are masked where consumed).  Unconditional: tile 0 gets an offset
+  // past the buffer range, which reads 0.  Neither a select on the loaded data
+  // nor a branch around the loads may appear here -- either makes the compiler
+  // wait for them (and for every older load and store) on the spot.
+  auto prefetch_x0 = [&](int ti) {
+    const uint32_t off = ti > 0 ? (row_of_lane() * cs_ds + (uint32_t)((ti - 1) * a.dstate)) * 4u : 0x80000000u;
+#pragma unroll
+    for (int q = 0; q < kN / 4; ++q) px0[q] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, off + 16 * q));
+  };
 
+#ifdef MC_BWD_STAMPS
+  uint64_t st_pro = 0, st_pair = 0, st_out = 0;
+#endif
   const int ntiles = (L_ + kTB - 1) / kTB;
-  prefetch(ntiles - 1);
-  for (int ti = ntiles - 1; ti >= 0; --ti) {
+  // mode 0: one tile at a time; 1 / 2: first (odd) / second (even) tile of a pair
+  auto tile_body = [&](const int ti, auto mode_c) {
+    constexpr int kMode = decltype(mode_c)::value;
+#ifdef MC_BWD_STAMPS
+    const uint64_t s0 = __builtin_amdgcn_s_memtime();
+#endif
     const int l0 = ti * kTB;
     const bool full = kAligned && (l0 + kTB <= L_);
-    __syncthreads();                             // previous tile is done with the B/C quads
+    wave_lds_sync();                             // previous tile is done with the B/C quads
 #pragma unroll
     for (int k = 0; k < kBCPer; ++k) {
       const int q = lane + k * kRows;
-      if (q < kBCQ) bcq[q] = pbc[k];
+      if ((k + 1) * kRows <= kBCQ || q < kBCQ) bcq[q] = pbc[k];
     }
     // this tile's per-position scalars (from the prefetched raw rows)
     float dt[kTB], dtu[kTB], gy[kTB];
 #pragma unroll
     for (int t = 0; t < kTB; ++t) {
-      const float uv = elem_f<TI>(ru[t / VI], t % VI);
+      // positions past L (ragged first tile) hold whatever the 16-B loads
+      // returned: zero them before they meet the recurrence
+      const bool tv = full || l0 + t < L_;
+      const float uv = tv ? elem_f<TI>(ru[t / VI], t % VI) : 0.f;
       const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
-      const float go = elem_f<TI>(rg[t / VI], t % VI);
+      const float go = tv ? elem_f<TI>(rg[t / VI], t % VI) : 0.f;
       float d = softplus ? softplus_f(r) : r;
-      d = (l0 + t < L_) ? d : 0.f;
+      d = tv ? d : 0.f;
       dt[t] = d;
-      dtu[t] = d * uv;
+      // lanes mirroring a row past the group end: dtu = gy = 0 zeroes their
+      // dB / dC contributions here, once per tile, instead of a select per
+      // value in every pair's reductions (their own outputs are never stored)
+      dtu[t] = my_ok ? d * uv : 0.f;
       if (hasZ) {
-        const float zv = elem_f<TI>(rz[t / VI], t % VI);
-        gy[t] = go * zv * sigmoid_f(zv);          // dout * silu(z)
+        const float zv = tv ? elem_f<TI>(rz[t / VI], t % VI) : 0.f;
+        gy[t] = my_ok ? go * zv * sigmoid_f(zv) : 0.f;   // dout * silu(z)
       } else {
-        gy[t] = go;
+        gy[t] = my_ok ? go : 0.f;
       }
     }
-    // saved state at the tile start -> LDS (its latency overlaps the prep math and the barrier)
+    // saved state at the tile start -> LDS
 #pragma unroll
-    for (int p = 0; p < kP; ++p) {
-      f32x2 v = {0.f, 0.f};
-      if (ti > 0) {
-        const float* cs = csrow + (int64_t)(ti - 1) * a.dstate;
-        if ((a.dstate & 1) == 0) {
-          if (2 * p < a.dstate) v = *reinterpret_cast<const f32x2*>(cs + 2 * p);
-        } else {
-          if (2 * p < a.dstate) v.x = cs[2 * p];
-          if (2 * p + 1 < a.dstate) v.y = cs[2 * p + 1];
-        }
-      }
-      x0_s[p * kRows + lane] = v;
+    for (int q = 0; q < kN / 4; ++q) {
+      const f32x4 v = px0[q];
+      x0_s[(2 * q) * kRows + lane] = f32x2{4 * q < a.dstate ? v.x : 0.f, 4 * q + 1 < a.dstate ? v.y : 0.f};
+      x0_s[(2 * q + 1) * kRows + lane] = f32x2{4 * q + 2 < a.dstate ? v.z : 0.f, 4 * q + 3 < a.dstate ? v.w : 0.f};
     }
-    __syncthreads();                             // B/C quads staged
-    if (ti > 0) prefetch(ti - 1);                // next tile's loads fly under this tile's math
-
-    f32x2 Y2[kTB], S2[kTB], Q2[kTB];
+    wave_lds_sync();                             // B/C quads staged
+    // next tile's loads fly under this tile's math.  kAligned: unconditional
+    // (tile -1 addresses land outside the buffers or in unused row bytes)
+    if constexpr (kMode == 0) {
+      if (kAligned || ti > 0) load_rows(ti - 1, kAligned, ru, rd, rz, rg);
+    } else if constexpr (kMode == 1) {
 #pragma unroll
-    for (int t = 0; t < kTB; ++t) { Y2[t] = f32x2{0.f, 0.f}; S2[t] = f32x2{0.f, 0.f}; Q2[t] = f32x2{0.f, 0.f}; }
+      for (int k = 0; k < kVT; ++k) { ru[k] = su[k]; rd[k] = sd[k]; rz[k] = sz[k]; rg[k] = sg[k]; }
+    } else {
+      load_rows(ti - 1, true, ru, rd, rz, rg);   // tile -1 / -2 addresses land outside the
+      load_rows(ti - 2, true, su, sd, sz, sg);   // buffers or in unused row bytes
+    }
+    prefetch_bc(ti - 1);
+    prefetch_x0(ti - 1);
+    // the forward's pre-gate y of this tile (dz only), consumed after the pair loop
+    uint4 cy[kVT];
+    tile_in(rs_y, yb, yds64, l0, full, cy);
 
+    f32x2 S2[kTB], Q2[kTB];
+#pragma unroll
+    for (int t = 0; t < kTB; ++t) { S2[t] = f32x2{0.f, 0.f}; Q2[t] = f32x2{0.f, 0.f}; }
+
+#ifdef MC_BWD_STAMPS
+    const uint64_t s1 = __builtin_amdgcn_s_memtime();
+    st_pro += s1 - s0;
+#endif
 #pragma unroll 1
     for (int p = 0; p < kP; ++p) {
       const f32x2 A2p = a2_s[p * kRows + lane];
@@ -299,28 +434,42 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
 #pragma unroll
       for (int t = 0; t < kTB; ++t) {
         const f32x2 arg = A2p * dt[t];
+#ifdef MC_DIAG_NOEXP
+        const f32x2 aa = arg;
+#else
         const f32x2 aa = {fast_exp2(arg.x), fast_exp2(arg.y)};
+#endif
         x = aa * x + bc[t].lo * dtu[t];
         xs[t] = x;
         as[t] = aa;
-        Y2[t] = bc[t].hi * x + Y2[t];
       }
       // dC_t,n = sum over the wave's channels of gy_t x_t,n
       {
         float red[2 * kTB];
 #pragma unroll
         for (int t = 0; t < kTB; ++t) {
-          const f32x2 v = my_ok ? xs[t] * gy[t] : f32x2{0.f, 0.f};
+          const f32x2 v = xs[t] * gy[t];
           red[2 * t] = v.x;
           red[2 * t + 1] = v.y;
         }
+#ifdef MC_DIAG_NORED
+        float tot = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2 * kTB; ++i) tot += red[i];
+#else
         const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+#endif
         const int j = lane / (64 / (2 * kTB));
         const int t = j / 2, n = 2 * p + (j & 1);
-        if ((lane & (64 / (2 * kTB) - 1)) == 0 && n < a.dstate && l0 + t < L_)
-          a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 1) * L_ + l0 + t] = tot;
+        if ((lane & (64 / (2 * kTB) - 1)) == 0)
+          dbc_s[(t * 2 + 1) * kN + n] = tot;
       }
-      // reverse sweep: adjoint of the state
+      // reverse sweep: adjoint of the state.  The B/C quads are read from LDS
+      // again (the compiler barrier stops them being kept live across the dC
+      // reduction: 32 VGPRs at the kernel's pressure peak)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < kTB; ++t) bc[t] = bcq[p * kTB + t];
       f32x2 h = carry_s[p * kRows + lane];
       f32x2 dAp = dA_s[p * kRows + lane];
       float red[2 * kTB];
@@ -328,7 +477,7 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
       for (int t = kTB - 1; t >= 0; --t) {
         h = bc[t].hi * gy[t] + h;                  // + C_t gy_t
         S2[t] = h * bc[t].lo + S2[t];
-        const f32x2 vb = my_ok ? h * dtu[t] : f32x2{0.f, 0.f};
+        const f32x2 vb = h * dtu[t];
         red[2 * t] = vb.x;
         red[2 * t + 1] = vb.y;
         const f32x2 ha = h * as[t];
@@ -340,20 +489,43 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
       carry_s[p * kRows + lane] = h;
       dA_s[p * kRows + lane] = dAp;
       {
+#ifdef MC_DIAG_NORED
+        float tot = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2 * kTB; ++i) tot += red[i];
+#else
         const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+#endif
         const int j = lane / (64 / (2 * kTB));
         const int t = j / 2, n = 2 * p + (j & 1);
-        if ((lane & (64 / (2 * kTB) - 1)) == 0 && n < a.dstate && l0 + t < L_)
-          a.slab_bc[((((int64_t)bg * a.nblk + dblk) * kN + n) * 2 + 0) * L_ + l0 + t] = tot;
+        if ((lane & (64 / (2 * kTB) - 1)) == 0)
+          dbc_s[(t * 2 + 0) * kN + n] = tot;
       }
     }
 
-    // ---- per-position outputs of my channel (this tile's rows re-read: L2 hits)
+#ifdef MC_BWD_STAMPS
+    const uint64_t s2 = __builtin_amdgcn_s_memtime();
+    st_pair += s2 - s1;
+#endif
+    // ---- the tile's dB / dC sums: one coalesced 16-B store per lane into
+    // this wave's slab block (positions past L fall outside the buffer range
+    // and are dropped)
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < (kTB * 2 * kN) / (4 * kRows) + ((kTB * 2 * kN) % (4 * kRows) ? 1 : 0); ++k) {
+      const int f = 4 * (lane + k * kRows);
+      if (f < kTB * 2 * kN) {
+        const uint4 v = *reinterpret_cast<const uint4*>(dbc_s + f);
+        buf_st16(rs_slab, (uint32_t)((l0 * 2 * kN + f) * 4), v);
+      }
+    }
+    // ---- per-position outputs of my channel (this tile's rows re-read: L2
+    // hits; keeping them in registers through the pair loop would spill)
     uint4 cu[kVT], cd[kVT], cz[kVT], cg[kVT];
-    load_row_tile<TI>(urow, l0, L_, full, cu);
-    load_row_tile<TI>(drow, l0, L_, full, cd);
-    if (hasZ) load_row_tile<TI>(zrow, l0, L_, full, cz);
-    load_row_tile<TI>(grow, l0, L_, full, cg);
+    tile_in(rs_u, ub, a.u_ds, l0, full, cu);
+    tile_in(rs_d, db, a.dt_ds, l0, full, cd);
+    tile_in(rs_z, zb, zds64, l0, full, cz);
+    tile_in(rs_g, gb, a.go_ds, l0, full, cg);
     float o_du[kTB], o_dd[kTB], o_dz[kTB];
 #pragma unroll
     for (int t = 0; t < kTB; ++t) {
@@ -362,7 +534,6 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
       const float go = elem_f<TI>(cg[t / VI], t % VI);
       const float S = S2[t].x + S2[t].y;
       const float Q = (Q2[t].x + Q2[t].y) * kLn2;   // A2 carries log2(e)
-      const float y = fmaf(Dv, uv, Y2[t].x + Y2[t].y);
       const float sg = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
       float gyv = go;
       float gz = 0.f;
@@ -372,7 +543,7 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
         gyv = go * zv * sgz;
         gz = go * sgz * (1.f + zv * (1.f - sgz));
       }
-      o_dz[t] = gz * y;
+      o_dz[t] = gz * elem_f<TI>(cy[t / VI], t % VI);   // y + D u, as the forward produced it
       o_du[t] = fmaf(Dv, gyv, dt[t] * S);
       const float dr = fmaf(uv, S, Q) * sg;
       o_dd[t] = dr;
@@ -382,11 +553,45 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
       }
     }
     if (my_ok) {
-      store_row_tile<TI>(durow, l0, L_, full, o_du);
-      store_row_tile<TI>(ddrow, l0, L_, full, o_dd);
-      if (hasZ) store_row_tile<TI>(dzrow, l0, L_, full, o_dz);
+      const uint32_t rl = row_of_lane();
+      tile_out(rs_du, dub, a.du_ds, rl, l0, full, o_du);
+      tile_out(rs_dd, ddb, a.ddt_ds, rl, l0, full, o_dd);
+      if (hasZ) tile_out(rs_dz, dzb, a.dz_ds, rl, l0, full, o_dz);
     }
+#ifdef MC_BWD_STAMPS
+    st_out += __builtin_amdgcn_s_memtime() - s2;
+#endif
+  };
+
+  // drain once before the loop: the loop header then merges "nothing pending"
+  // from the entry edge, so consuming a prefetch never waits for the previous
+  // tile's stores (vmcnt counts stores too on gfx9)
+  if constexpr (kPairs) {
+    const int npairs = (ntiles + 1) / 2;     // an odd tile count adds one tile past L (fully masked)
+    load_rows(2 * npairs - 1, true, ru, rd, rz, rg);
+    load_rows(2 * npairs - 2, true, su, sd, sz, sg);
+    prefetch_bc(2 * npairs - 1);
+    prefetch_x0(2 * npairs - 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    for (int k = npairs - 1; k >= 0; --k) {
+      tile_body(2 * k + 1, std::integral_constant<int, 1>());
+      tile_body(2 * k, std::integral_constant<int, 2>());
+    }
+  } else {
+    load_rows(ntiles - 1, kAligned && ntiles * kTB <= L_, ru, rd, rz, rg);
+    prefetch_bc(ntiles - 1);
+    prefetch_x0(ntiles - 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    for (int ti = ntiles - 1; ti >= 0; --ti) tile_body(ti, std::integral_constant<int, 0>());
   }
+#ifdef MC_BWD_STAMPS
+  // diagnostic build: per-wave segment cycles -> slab_d (outputs are invalid in this build)
+  if (lane == 0) {
+    uint64_t* dbg = reinterpret_cast<uint64_t*>(a.slab_d) + (int64_t)blockIdx.x * 4;
+    dbg[0] = st_pro; dbg[1] = st_pair; dbg[2] = st_out; dbg[3] = ntiles;
+  }
+  return;
+#endif
 
   if (my_ok) {
     // slab_a is [b][n][d]: coalesced along d
@@ -405,16 +610,18 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
 template <typename TW, int kN>
 __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, int G, int nblk,
                                                            int dstate, int L, TW* __restrict__ dB, TW* __restrict__ dC) {
-  const int64_t total = (int64_t)batch * G * dstate * 2 * L;
+  // thread -> (b*G+g, l, which, n), n fastest: the slab reads are coalesced
+  const int64_t total = (int64_t)batch * G * L * 2 * kN;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int l = (int)(i % L);
-    int64_t r = i / L;
+    const int n = (int)(i % kN);
+    int64_t r = i / kN;
     const int which = (int)(r % 2);
     r /= 2;
-    const int n = (int)(r % dstate);
-    const int64_t bgi = r / dstate;
+    const int l = (int)(r % L);
+    const int64_t bgi = r / L;
+    if (n >= dstate) continue;
     float s = 0.f;
-    for (int k = 0; k < nblk; ++k) s += slab[(((bgi * nblk + k) * kN + n) * 2 + which) * L + l];
+    for (int k = 0; k < nblk; ++k) s += slab[((bgi * nblk + k) * L + l) * (2 * kN) + which * kN + n];
     TW* dst = which ? dC : dB;
     dst[(bgi * dstate + n) * L + l] = from_f<TW>(s);
   }
@@ -486,7 +693,8 @@ static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
 
 template <typename TI, int kN>
 static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
-  const size_t lds = (size_t)(kN / 2) * kTB * 16 + (size_t)4 * (kN / 2) * kRows * 8;   // B/C quads + carry, dA, x0, A
+  // B/C quads + carry, dA, x0, A + the tile's dB / dC sums
+  const size_t lds = (size_t)(kN / 2) * kTB * 16 + (size_t)4 * (kN / 2) * kRows * 8 + (size_t)kTB * 2 * kN * 4;
   if (aligned)
     hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else
@@ -506,7 +714,7 @@ static int launch_bwd_t(const BwdArgs& a, bool aligned, hipStream_t s) {
 
 template <typename TW, int kN>
 static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float* dD, float* dbias, hipStream_t s) {
-  const int64_t total = (int64_t)a.batch * a.n_groups * a.dstate * 2 * a.seqlen;
+  const int64_t total = (int64_t)a.batch * a.n_groups * kN * 2 * a.seqlen;
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL((scan_bwd_reduce_bc<TW, kN>), dim3(grid), dim3(256), 0, s, a.slab_bc, a.batch, a.n_groups,
                      a.nblk, a.dstate, a.seqlen, reinterpret_cast<TW*>(dB), reinterpret_cast<TW*>(dC));
@@ -560,7 +768,10 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   }
   MC_CHECK(p->u && p->delta && p->B && p->C && p->dout && p->du && p->ddelta && p->dB && p->dC, MC_ERR_INVALID,
            "mc_scan_bwd: u, delta, B, C, dout and du, ddelta, dB, dC must be non-null");
-  MC_CHECK(!p->z || p->dz, MC_ERR_INVALID, "mc_scan_bwd: dz required when z is given");
+  MC_CHECK(!p->z || (p->dz && p->out_y), MC_ERR_INVALID,
+           "mc_scan_bwd: dz and out_y (the forward's pre-gate output) required when z is given");
+  MC_CHECK((int64_t)kRows * mc_scan_n_chunks(p->seqlen) * padded_dstate(p->dstate) * 4 < ((int64_t)1 << 31),
+           MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit chunk-state offsets", p->seqlen);
   MC_CHECK(p->chunk_states, MC_ERR_INVALID, "mc_scan_bwd: chunk_states (from the training forward) required");
   const BwdWs w = bwd_ws_layout(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups);
   MC_CHECK(p->workspace && p->workspace_bytes >= w.total && (reinterpret_cast<uintptr_t>(p->workspace) & 255) == 0,
@@ -590,6 +801,7 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   a.du_bs = p->du_batch_stride; a.du_ds = p->du_dim_stride;
   a.ddt_bs = p->ddelta_batch_stride; a.ddt_ds = p->ddelta_dim_stride;
   a.dz_bs = p->dz_batch_stride; a.dz_ds = p->dz_dim_stride;
+  a.y = p->z ? p->out_y : nullptr; a.y_bs = p->out_y_batch_stride; a.y_ds = p->out_y_dim_stride;
   a.slab_bc = reinterpret_cast<float*>(ws + w.slab_bc);
   a.slab_a = reinterpret_cast<float*>(ws + w.slab_a);
   a.slab_d = reinterpret_cast<float*>(ws + w.slab_d);
@@ -598,13 +810,23 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   // outputs are contiguous: the vector path also needs 16-B aligned rows there
-  const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
+  bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
                        vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
                        vec_ok(p->dout, p->dout_batch_stride, p->dout_dim_stride, 0, ib) &&
                        vec_ok(p->du, p->du_batch_stride, p->du_dim_stride, 0, ib) &&
                        vec_ok(p->ddelta, p->ddelta_batch_stride, p->ddelta_dim_stride, 0, ib) &&
-                       vec_ok(p->dz, p->dz_batch_stride, p->dz_dim_stride, 0, ib);
+                       vec_ok(p->dz, p->dz_batch_stride, p->dz_dim_stride, 0, ib) &&
+                       vec_ok(a.y, a.y_bs, a.y_ds, 0, ib);
+  // the vector path addresses a wave's 64 rows with 32-bit byte offsets
+  auto span_ok = [&](const void* t, int64_t ds) {
+    return !t || ((int64_t)(kRows - 1) * (ds < 0 ? -ds : ds) + p->seqlen) * ib < ((int64_t)1 << 31);
+  };
+  const bool spans = span_ok(p->u, p->u_dim_stride) && span_ok(p->delta, p->delta_dim_stride) &&
+                     span_ok(p->z, p->z_dim_stride) && span_ok(p->dout, p->dout_dim_stride) &&
+                     span_ok(p->du, p->du_dim_stride) && span_ok(p->ddelta, p->ddelta_dim_stride) &&
+                     span_ok(p->dz, p->dz_dim_stride) && span_ok(a.y, a.y_ds);
+  aligned = aligned && spans;
   if (p->itype == MC_DTYPE_F32) rc = launch_bwd_t<float>(a, aligned, s);
   else if (p->itype == MC_DTYPE_BF16) rc = launch_bwd_t<bf16_t>(a, aligned, s);
   else rc = launch_bwd_t<f16_t>(a, aligned, s);

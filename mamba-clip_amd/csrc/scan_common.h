@@ -22,6 +22,23 @@ inline size_t bct_bytes(int batch, int seqlen, int dstate, int n_groups) {
   return (size_t)batch * n_groups * seqlen * 2 * padded_dstate(dstate) * sizeof(float);
 }
 
+// LDS hand-off between the lanes of a ONE-WAVE workgroup.  A wave's LDS
+// instructions are performed in program order, so a compiler barrier is all
+// the ordering a cross-lane exchange needs.  __syncthreads() would also lower
+// to a vmcnt(0)/lgkmcnt(0) drain: every chunk would wait for the previous
+// chunk's global stores and for prefetch loads still in flight (measured in
+// the backward: ~2/3 of the wave's cycles sat in those drains).
+static_assert(kRows == 64, "wave_lds_sync() is only valid for one-wave workgroups");
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
+
+// Lane id the compiler cannot hoist or CSE (asm volatile): values derived from
+// it are rebuilt where used instead of occupying VGPRs across a hot loop.
+__device__ __forceinline__ int opaque_lane_id() {
+  int v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
+}
+
 // Bijective blockIdx remap so that consecutive logical blocks (same batch /
 // group, sharing B/C) run on one XCD: hardware deals blocks round-robin over
 // the 8 XCDs (speed only -- correctness never depends on placement).

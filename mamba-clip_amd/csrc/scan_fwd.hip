@@ -38,6 +38,7 @@ struct FwdArgs {
   const void* u; const void* delta; const float* A; const float* bct;
   const float* D; const void* z; const float* delta_bias;
   void* out; float* chunk_states; float* last_state;
+  void* out_y; int64_t y_bs, y_ds;   // nullable: pre-gate y + D u (training with z: the backward's dz input)
 };
 
 // Variants (template knobs, chosen on the host):
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
         if (v < kBCVec) reinterpret_cast<float4*>(bcl)[v] = cur[k];
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     if constexpr (kPU) {
       if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
     }
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
         }
       }
     }
-    __syncthreads();
+    wave_lds_sync();
 
     // ---- gate + store, coalesced along the sequence (same vector mapping)
 #pragma unroll
@@ -267,6 +268,12 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
         o[e] = reinterpret_cast<const float*>(ie < kG / 2 ? pu : pu + 16)[ie % (kG / 2)];
       }
       if (hasZ) {
+        if (a.out_y && r < nrows) {
+          TI* ydst = reinterpret_cast<TI*>(a.out_y) + (int64_t)b * a.y_bs + (int64_t)(dbase + r) * a.y_ds + col0;
+          const uint4 yq = pack_f<TI>(o);
+          if (full) st16(ydst, yq);
+          else st16_masked(ydst, yq, nv);
+        }
         const TI* zs = zp + (int64_t)(dbase + min(r, nrows - 1)) * a.z_ds + col0;
         const uint4 zq = full ? ld16(zs) : ld16_masked(zs, nv);
 #pragma unroll
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
         else st16_masked(dst, ov, nv);
       }
     }
-    __syncthreads();  // next chunk's staging overwrites the rows
+    wave_lds_sync();  // next chunk's staging overwrites the rows
   }
 
   if (a.last_state && my_ok) {
@@ -410,7 +417,7 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
     uint4 cz[kVL];
 #pragma unroll
     for (int k = 0; k < kVL; ++k) cz[k] = pz[k];
-    __syncthreads();
+    wave_lds_sync();
     uint4 ru[kR][kVPR], rd[kR][kVPR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
       step(tt, bcA, bcB);
       step(tt + 1, bcB, bcA);
     }
-    __syncthreads();
+    wave_lds_sync();
 
     // ---- gate + store, coalesced along the sequence (z prefetched a chunk ago)
 #pragma unroll
@@ -495,6 +502,12 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
         o[4 * e4] = q.x; o[4 * e4 + 1] = q.y; o[4 * e4 + 2] = q.z; o[4 * e4 + 3] = q.w;
       }
       if (hasZ) {
+        if (a.out_y && r < nrows) {
+          TI* ydst = reinterpret_cast<TI*>(a.out_y) + (int64_t)b * a.y_bs + (int64_t)(dbase + r) * a.y_ds + col0;
+          const uint4 yq = pack_f<TI>(o);
+          if (full) st16(ydst, yq);
+          else st16_masked(ydst, yq, nv);
+        }
 #pragma unroll
         for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(cz[k], e));
       }
@@ -505,7 +518,7 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
         else st16_masked(dst, ov, nv);
       }
     }
-    __syncthreads();
+    wave_lds_sync();
   }
 
 #pragma unroll
@@ -663,12 +676,14 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   a.u = p->u; a.delta = p->delta; a.A = p->A; a.bct = reinterpret_cast<const float*>(p->workspace);
   a.D = p->D; a.z = p->z; a.delta_bias = p->delta_bias;
   a.out = p->out; a.chunk_states = p->chunk_states; a.last_state = p->last_state;
+  a.out_y = p->z ? p->out_y : nullptr; a.y_bs = p->out_y_batch_stride; a.y_ds = p->out_y_dim_stride;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
                        vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
-                       vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib);
+                       vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
+                       vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
   return launch_fwd_t<f16_t>(a, aligned, s);

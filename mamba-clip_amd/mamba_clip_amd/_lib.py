@@ -33,6 +33,7 @@ class ScanFwdParams(ctypes.Structure):
         ("D", c_fp), ("z", c_vp), ("delta_bias", c_fp),
         ("out", c_vp), ("chunk_states", c_fp), ("last_state", c_fp),
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+        ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
     ]
 
 
@@ -55,6 +56,7 @@ class ScanBwdParams(ctypes.Structure):
         ("du", c_vp), ("ddelta", c_vp), ("dz", c_vp), ("dB", c_vp), ("dC", c_vp),
         ("dA", c_fp), ("dD", c_fp), ("ddelta_bias", c_fp),
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+        ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
     ]
 
 

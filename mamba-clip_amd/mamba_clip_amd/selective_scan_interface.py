@@ -56,8 +56,13 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
         raise RuntimeError("selective_scan_fn: dim must be divisible by n_groups")
 
 
-def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last):
-    """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None)."""
+def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False):
+    """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None[, out_y]).
+
+    ``want_y`` (training with z): also return the pre-gate output y + D u that
+    the backward's dz needs -- upstream's forward returns it as ``out`` next to
+    ``out_z``.
+    """
     lib = _lib.load()
     batch, dim, L = u.shape
     dstate = A.shape[1]
@@ -85,13 +90,18 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     ws_bytes = lib.mc_scan_fwd_workspace_bytes(batch, L, dstate, G)
     ws = torch.empty(max(ws_bytes, 1), device=u.device, dtype=torch.uint8)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
+    out_y = torch.empty_like(u) if (want_y and z is not None) else None
+    if out_y is not None:
+        p.out_y, p.out_y_batch_stride, p.out_y_dim_stride = out_y.data_ptr(), out_y.stride(0), out_y.stride(1)
     _lib.check(lib.mc_scan_fwd(p, _lib.stream_handle(u.device)), "mc_scan_fwd")
     if want_last and states is not None:
         last = states[:, :, -1, :] if nch > 0 else torch.zeros(batch, dim, dstate, device=u.device)
+    if want_y:
+        return out, states, last, out_y
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, out_y=None):
     lib = _lib.load()
     batch, dim, L = u.shape
     dstate = A.shape[1]
@@ -128,6 +138,8 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
     p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
     p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
+    if out_y is not None:
+        p.out_y, p.out_y_batch_stride, p.out_y_dim_stride = out_y.data_ptr(), out_y.stride(0), out_y.stride(1)
     _lib.check(lib.mc_scan_bwd(p, _lib.stream_handle(u.device)), "mc_scan_bwd")
     return du, ddelta, dA, dB, dC, dD, dz, dbias
 
@@ -146,10 +158,12 @@ class SelectiveScanFn(torch.autograd.Function):
         bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
         _check_inputs(u, delta, A32, B, C, D32, z, bias32)
         need_grad = any(ctx.needs_input_grad[:8])
-        out, states, last = scan_fwd(u, delta, A32, B, C, D32, z, bias32, delta_softplus,
-                                     want_states=need_grad, want_last=return_last_state)
+        res = scan_fwd(u, delta, A32, B, C, D32, z, bias32, delta_softplus,
+                       want_states=need_grad, want_last=return_last_state, want_y=need_grad)
+        out, states, last = res[:3]
+        out_y = res[3] if need_grad else None
         if need_grad:
-            ctx.save_for_backward(u, delta, A32, B, C, D32, z, bias32, states)
+            ctx.save_for_backward(u, delta, A32, B, C, D32, z, bias32, states, out_y)
         ctx.delta_softplus = delta_softplus
         ctx.squeeze = (squeeze_B, squeeze_C)
         ctx.dtypes = (A.dtype, D.dtype if D is not None else None,
@@ -159,9 +173,9 @@ class SelectiveScanFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, *args):
-        u, delta, A32, B, C, D32, z, bias32, states = ctx.saved_tensors
+        u, delta, A32, B, C, D32, z, bias32, states, out_y = ctx.saved_tensors
         du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, delta, A32, B, C, D32, z, bias32,
-                                                         ctx.delta_softplus, dout, states)
+                                                         ctx.delta_softplus, dout, states, out_y)
         if ctx.squeeze[0]:
             dB = dB.squeeze(1)
         if ctx.squeeze[1]:
