@@ -73,6 +73,10 @@ CASES = [
     (2, 128, 33, 8, 4, torch.float16, torch.float32, True, False),         # f16 / fp32 B,C, N=8
     (1, 64, 250, 32, 1, torch.float32, torch.bfloat16, True, False),       # N=32
     (3, 96, 5, 3, 3, torch.bfloat16, torch.float32, False, False),         # odd N, tiny L
+    # 16-B aligned 16-bit rows take the backward's paired-tile path; odd tile counts
+    # add one fully masked tile past L
+    (2, 192, 40, 16, 1, torch.bfloat16, torch.bfloat16, True, False),      # 5 tiles (odd)
+    (2, 128, 24, 16, 2, torch.float16, torch.bfloat16, False, False),      # 3 tiles, no z, G=2
 ]
 
 
@@ -204,6 +208,36 @@ def test_scan_bwd_random_vs_oracle(case):
     x = _rand_case(batch, dim, L, N, G, it, wt, z=z, three_d=three_d, seed=batch * 11 + dim)
     dout = torch.randn(batch, dim, L, generator=torch.Generator().manual_seed(3))
     _check_backward(x, True, dout, it)
+
+
+@pytest.mark.parametrize("L", [35, 41])
+def test_scan_bwd_ragged_aligned_rows(L):
+    """Inputs are views into rows padded to 48 (16-B aligned) with a ragged L
+    (L=35: 5 tiles, L=41: 6 tiles).  The gradients are allocated dense, so
+    their rows are not 16-B aligned and the backward takes its element-wise
+    path.  Gradients reach the padded leaves through the views, and the
+    padding stays untouched."""
+    selective_scan_fn = _lib_fn()
+    x = _rand_case(2, 192, L, 16, 1, torch.bfloat16, torch.bfloat16, seed=L)
+    pads = {}
+    for k in ("u", "delta", "z"):
+        big = torch.zeros(2, 192, 48, dtype=torch.bfloat16)
+        big[:, :, :L] = x[k]
+        pads[k] = big.to(DEV).requires_grad_(True)
+    leaves = {k: (v.to(DEV).detach().requires_grad_(True) if v is not None else None)
+              for k, v in x.items() if k not in pads}
+    views = {k: pads[k][:, :, :L] for k in pads}
+    assert views["u"].stride(1) == 48
+    dout = torch.randn(2, 192, L, generator=torch.Generator().manual_seed(4))
+    out = selective_scan_fn(**views, **leaves, delta_softplus=True)
+    out.backward(dout.to(DEV).to(out.dtype))
+    ref = selective_scan_ref_grads(**x, delta_softplus=True, dout=dout.to(torch.bfloat16).double(),
+                                   compute_dtype=torch.float64)
+    for k, g in ref.items():
+        got = pads[k].grad[:, :, :L] if k in pads else leaves[k].grad
+        assert_grad_close(got, g, torch.bfloat16 if k in ("u", "delta", "z", "B", "C") else torch.float32, k)
+    for k in pads:
+        assert torch.count_nonzero(pads[k].grad[:, :, L:]) == 0, k
 
 
 def test_scan_bwd_deterministic():
