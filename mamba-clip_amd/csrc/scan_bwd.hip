@@ -160,8 +160,8 @@ __device__ __forceinline__ void store_row_tile(TI* __restrict__ base, uint32_t o
 // block is staged in LDS as [pair][position]{B_n, B_n+1, C_n, C_n+1} so one
 // broadcast ds_read_b128 serves a (pair, position).  The next tile's rows,
 // B/C block and saved state are prefetched into registers under this tile.
-template <typename TI, int kN, bool kAligned>
-__global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
+template <typename TI, int kN, bool kAligned, int kGrp>
+__global__ __launch_bounds__(kRows, kGrp >= 4 ? 1 : 2) void scan_bwd_kernel(const BwdArgs a) {
   constexpr int VI = ElemTraits<TI>::kVec;
   constexpr int kVT = kTB / VI;            // 16-B vectors per row tile (1 for 16-bit, 2 for fp32)
   constexpr int kP = kN / 2;               // state pairs
@@ -307,11 +307,13 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   // compiles to unconditional 16-B loads -- no control flow around the loads,
   // so nothing forces a vmcnt wait before the loads are consumed a tile later.
   uint4 ru[kVT], rd[kVT], rz[kVT], rg[kVT];
-  // 16-bit inputs: rows are fetched for TWO tiles at a time (the loads of
-  // both go out back to back, so each 128-B line a lane touches is fetched
-  // once for 16 positions instead of once per 8); the second tile waits here
-  constexpr bool kPairs = kAligned && sizeof(TI) == 2;
-  uint4 su[kVT], sd[kVT], sz[kVT], sg[kVT];
+  // 16-bit inputs: rows are fetched for a GROUP of kG tiles at a time (the
+  // loads go out back to back, so each 128-B line a lane touches is fetched
+  // once per 8 kG positions instead of once per 8); the later tiles of the
+  // group wait in su.. (kG = 4 runs at one wave per SIMD for the registers)
+  constexpr int kG = (kAligned && sizeof(TI) == 2) ? kGrp : 1;
+  constexpr int kS = kG > 1 ? kG - 1 : 1;
+  uint4 su[kS][kVT], sd[kS][kVT], sz[kS][kVT], sg[kS][kVT];
   f32x4 pbc[kBCPer];
   f32x4 px0[kN / 4];
   auto load_rows = [&](int ti, bool full, uint4 (&qu)[kVT], uint4 (&qd)[kVT], uint4 (&qz)[kVT], uint4 (&qg)[kVT]) {
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   uint64_t st_pro = 0, st_pair = 0, st_out = 0;
 #endif
   const int ntiles = (L_ + kTB - 1) / kTB;
-  // mode 0: one tile at a time; 1 / 2: first (odd) / second (even) tile of a pair
+  // mode -1: one tile at a time; m >= 0: the m-th tile (from the top) of a group
   auto tile_body = [&](const int ti, auto mode_c) {
     constexpr int kMode = decltype(mode_c)::value;
 #ifdef MC_BWD_STAMPS
@@ -398,14 +400,17 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
     wave_lds_sync();                             // B/C quads staged
     // next tile's loads fly under this tile's math.  kAligned: unconditional
     // (tile -1 addresses land outside the buffers or in unused row bytes)
-    if constexpr (kMode == 0) {
+    if constexpr (kMode < 0) {
       if (kAligned || ti > 0) load_rows(ti - 1, kAligned, ru, rd, rz, rg);
-    } else if constexpr (kMode == 1) {
+    } else if constexpr (kMode < kG - 1) {     // next tile of the group is already here
 #pragma unroll
-      for (int k = 0; k < kVT; ++k) { ru[k] = su[k]; rd[k] = sd[k]; rz[k] = sz[k]; rg[k] = sg[k]; }
-    } else {
-      load_rows(ti - 1, true, ru, rd, rz, rg);   // tile -1 / -2 addresses land outside the
-      load_rows(ti - 2, true, su, sd, sz, sg);   // buffers or in unused row bytes
+      for (int k = 0; k < kVT; ++k) {
+        ru[k] = su[kMode][k]; rd[k] = sd[kMode][k]; rz[k] = sz[kMode][k]; rg[k] = sg[kMode][k];
+      }
+    } else {                                   // last tile of the group: fetch the next group
+      load_rows(ti - 1, true, ru, rd, rz, rg);   // (tiles below 0 land outside the buffers
+#pragma unroll                                 //  or in unused row bytes)
+      for (int j = 0; j < kG - 1; ++j) load_rows(ti - 2 - j, true, su[j], sd[j], sz[j], sg[j]);
     }
     prefetch_bc(ti - 1);
     prefetch_x0(ti - 1);
@@ -566,23 +571,28 @@ __global__ __launch_bounds__(kRows, 2) void scan_bwd_kernel(const BwdArgs a) {
   // drain once before the loop: the loop header then merges "nothing pending"
   // from the entry edge, so consuming a prefetch never waits for the previous
   // tile's stores (vmcnt counts stores too on gfx9)
-  if constexpr (kPairs) {
-    const int npairs = (ntiles + 1) / 2;     // an odd tile count adds one tile past L (fully masked)
-    load_rows(2 * npairs - 1, true, ru, rd, rz, rg);
-    load_rows(2 * npairs - 2, true, su, sd, sz, sg);
-    prefetch_bc(2 * npairs - 1);
-    prefetch_x0(2 * npairs - 1);
+  if constexpr (kG > 1) {
+    const int ngroups = (ntiles + kG - 1) / kG;   // a partial group adds tiles past L (fully masked)
+    const int top = kG * ngroups - 1;
+    load_rows(top, true, ru, rd, rz, rg);
+#pragma unroll
+    for (int j = 0; j < kG - 1; ++j) load_rows(top - 1 - j, true, su[j], sd[j], sz[j], sg[j]);
+    prefetch_bc(top);
+    prefetch_x0(top);
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int k = npairs - 1; k >= 0; --k) {
-      tile_body(2 * k + 1, std::integral_constant<int, 1>());
-      tile_body(2 * k, std::integral_constant<int, 2>());
+    for (int k = ngroups - 1; k >= 0; --k) {
+      const int t0 = kG * k + kG - 1;
+      tile_body(t0, std::integral_constant<int, 0>());
+      if constexpr (kG >= 2) tile_body(t0 - 1, std::integral_constant<int, 1>());
+      if constexpr (kG >= 3) tile_body(t0 - 2, std::integral_constant<int, 2>());
+      if constexpr (kG >= 4) tile_body(t0 - 3, std::integral_constant<int, 3>());
     }
   } else {
     load_rows(ntiles - 1, kAligned && ntiles * kTB <= L_, ru, rd, rz, rg);
     prefetch_bc(ntiles - 1);
     prefetch_x0(ntiles - 1);
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int ti = ntiles - 1; ti >= 0; --ti) tile_body(ti, std::integral_constant<int, 0>());
+    for (int ti = ntiles - 1; ti >= 0; --ti) tile_body(ti, std::integral_constant<int, -1>());
   }
 #ifdef MC_BWD_STAMPS
   // diagnostic build: per-wave segment cycles -> slab_d (outputs are invalid in this build)
@@ -695,10 +705,16 @@ template <typename TI, int kN>
 static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
   // B/C quads + carry, dA, x0, A + the tile's dB / dC sums
   const size_t lds = (size_t)(kN / 2) * kTB * 16 + (size_t)4 * (kN / 2) * kRows * 8 + (size_t)kTB * 2 * kN * 4;
-  if (aligned)
-    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  else
-    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  // 16-bit rows in groups of 2 tiles.  Groups of 4 (one wave per SIMD for the
+  // registers) measured slower: C2 780 vs 724 us contiguous, 810 vs 817 us
+  // with the mixer's channel-major views (tools/ab_scan_bwd.sh)
+  if (aligned && sizeof(TI) == 2) {
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, 2>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  } else if (aligned) {
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, 1>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, 1>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  }
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;

@@ -14,14 +14,24 @@ ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--noz", action="store_true")
 ap.add_argument("--bwd", action="store_true", help="time forward+backward (training) instead")
+ap.add_argument("--cm", action="store_true",
+                help="channel-major views like the Mamba mixer: (B, D, L) with strides (L, B*L, 1)")
 args = ap.parse_args()
 Bsz, D, L, N = map(int, args.shape.split(","))
 dt = {"bf16": torch.bfloat16, "f32": torch.float32}[args.dtype]
 dev = "cuda"
 torch.manual_seed(0)
-u = torch.randn(Bsz, D, L, device=dev, dtype=dt)
-delta = (0.5 * torch.randn(Bsz, D, L, device=dev)).to(dt)
-z = None if args.noz else torch.randn(Bsz, D, L, device=dev, dtype=dt)
+
+
+def act(scale=1.0):
+    if args.cm:
+        return (scale * torch.randn(D, Bsz, L, device=dev)).to(dt).transpose(0, 1)
+    return (scale * torch.randn(Bsz, D, L, device=dev)).to(dt)
+
+
+u = act()
+delta = act(0.5)
+z = None if args.noz else act()
 A = -torch.exp(torch.log(torch.arange(1, N + 1, dtype=torch.float32, device=dev)).repeat(D, 1))
 Bm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
 Cm = torch.randn(Bsz, 1, N, L, device=dev, dtype=dt)
@@ -30,7 +40,7 @@ bias = torch.rand(D, device=dev) * 4 - 5
 if args.bwd:
     for t in (u, delta, A, Bm, Cm, Dv, bias) + ((z,) if z is not None else ()):
         t.requires_grad_(True)
-    g_out = torch.randn(Bsz, D, L, device=dev, dtype=dt)
+    g_out = act()
 
 
 def step():
