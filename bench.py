@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (MI355X_MICROARCH.md)
 MFMA_BF16_DENSE_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+MFMA_FP8_DENSE_TFLOPS = 5000.0   # dense fp8 MFMA peak (no sparsity)
 C2_FLOP_PER_PAIR = 146e9         # fwd+bwd, SURVEY.md 8(d)
 
 
@@ -109,6 +110,52 @@ def scan_roofline(iters, warmup=3):
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+
+
+def similarity_c5(iters=20, warmup=3):
+    """Config 5 similarity matmul: gathered N = 1024 x 8 = 8192 frozen features, E = 512, fp8 MFMA.
+
+    Times (HIP events on the launch stream) the row-wise e4m3 quantisation of both
+    operands + the fp8 GEMM (fp32 logits), the fp8 GEMM alone, and the bf16 GEMM
+    on the same features for comparison.  Algorithmic work: 2*N*N*E flop; the fp32
+    logit write (N*N*4 B) is the HBM side of the roofline.
+    """
+    import torch
+    import torch.nn.functional as F
+    from mamba_clip_amd.ops import gemm_nt, quant_rows_fp8, similarity_fp8
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, e = 8192, 512
+    g = torch.Generator(device=dev).manual_seed(5)
+    I = F.normalize(torch.randn(n, e, device=dev, generator=g), dim=-1).bfloat16()
+    T = F.normalize(torch.randn(n, e, device=dev, generator=g), dim=-1).bfloat16()
+    scale = torch.tensor(100.0, device=dev)
+    qi, si = quant_rows_fp8(I)
+    qt, st = quant_rows_fp8(T)
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        t0.record(stream)
+        for _ in range(iters):
+            fn()
+        t1.record(stream)
+        torch.cuda.synchronize(dev)
+        return t0.elapsed_time(t1) / iters
+
+    ms_all = timed(lambda: similarity_fp8(I, T, scale))
+    ms_gemm = timed(lambda: gemm_nt(qi, qt, alpha_dev=scale, scale_a=si, scale_b=st))
+    ms_bf16 = timed(lambda: gemm_nt(I, T, alpha_dev=scale))
+    flop = 2.0 * n * n * e
+    tflops = flop / (ms_gemm * 1e-3) / 1e12
+    write_gbs = n * n * 4 / (ms_gemm * 1e-3) / 1e9
+    return {"kernel": "gemm_nt fp8 e4m3 (v_mfma_f32_16x16x32_fp8_fp8) @ C5 N=8192 E=512, fp32 logits",
+            "ms_quant_plus_gemm": round(ms_all, 4), "ms_gemm": round(ms_gemm, 4), "ms_gemm_bf16": round(ms_bf16, 4),
+            "achieved_tflops": round(tflops, 1), "peak_tflops_fp8_dense": MFMA_FP8_DENSE_TFLOPS,
+            "frac_mfma": round(tflops / MFMA_FP8_DENSE_TFLOPS, 4),
+            "logit_write_gbs": round(write_gbs, 1), "frac_hbm_write": round(write_gbs / HBM_PEAK_GBS, 4)}
 
 
 def _pmc_traffic():
@@ -218,6 +265,8 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and not args.no_roofline:
         result["roofline"] = scan_roofline(args.scan_iters)
+    if rank == 0 and not args.no_roofline:
+        result["similarity_fp8"] = similarity_c5()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.model)
     if world > 1:

@@ -26,11 +26,17 @@
 extern "C" {
 #endif
 
-/* C[m, n] = alpha * sum_k A[m, k] * B[n, k]   (A: M x K, B: N x K, K contiguous)
- * dtype of A and B: MC_DTYPE_BF16 (MFMA bf16, fp32 accumulate) or
- * MC_DTYPE_F32 (exact-fp32 MFMA).  alpha = *alpha_dev if alpha_dev != NULL
+/* C[m, n] = alpha * sa[m] * sb[n] * sum_k A[m, k] * B[n, k]   (A: M x K, B: N x K, K contiguous)
+ * dtype of A and B: MC_DTYPE_BF16 (MFMA bf16, fp32 accumulate),
+ * MC_DTYPE_F32 (exact-fp32 MFMA) or MC_DTYPE_FP8_E4M3 (fp8 MFMA, fp32
+ * accumulate; K, lda, ldb multiples of 16 and A, B 16-B aligned -- the
+ * quantiser below pads K).  alpha = *alpha_dev if alpha_dev != NULL
  * (a device scalar such as logit_scale.exp(): no host sync), else alpha.
- * C is fp32 (out_dtype MC_DTYPE_F32) or bf16 (MC_DTYPE_BF16). */
+ * sa / sb: optional per-row dequantisation factors of A / B (fp32, M / N
+ * entries; NULL = 1), as written by mc_quant_rows_fp8.
+ * C is fp32 (out_dtype MC_DTYPE_F32) or bf16 (MC_DTYPE_BF16).
+ * Replaces the similarity matmul of ClipModel.get_logits (model.py:1104-1112)
+ * and ClipLoss.get_logits (loss.py:89-113). */
 typedef struct mc_gemm_nt_params {
   int32_t M, N, K;
   int32_t in_dtype, out_dtype;
@@ -39,9 +45,22 @@ typedef struct mc_gemm_nt_params {
   void* C; int64_t ldc;
   float alpha;
   const float* alpha_dev;
+  const float* row_scale_a;
+  const float* row_scale_b;
 } mc_gemm_nt_params;
 
 int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream);
+
+/* Row-wise fp8 quantisation of a rows x cols matrix X (fp32 / bf16 / f16,
+ * leading dimension ldx) for the fp8 similarity GEMM (stage-2 / frozen
+ * features, BASELINE config 5):
+ *   amax_i = max_j |X[i, j]|,  s_i = 448 / amax_i  (1 if amax_i == 0)
+ *   Q[i, j] = e4m3fn_rne(clamp(X[i, j] * s_i, -448, 448))   for j < cols
+ *   Q[i, j] = 0                                           for cols <= j < ldq
+ *   inv_scale[i] = 1 / s_i
+ * ldq must be a multiple of 16 and >= cols; Q 16-B aligned. */
+int mc_quant_rows_fp8(int32_t rows, int32_t cols, int32_t in_dtype, const void* X, int64_t ldx, uint8_t* Q,
+                      int64_t ldq, float* inv_scale, void* stream);
 
 /* Softmax cross-entropy statistics along the rows (axis = 0: one value per
  * row, reduce over columns) or the columns (axis = 1) of an fp32 matrix S

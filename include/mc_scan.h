@@ -38,7 +38,8 @@ extern "C" {
 typedef enum mc_dtype {
   MC_DTYPE_F32 = 0,
   MC_DTYPE_BF16 = 1,
-  MC_DTYPE_F16 = 2
+  MC_DTYPE_F16 = 2,
+  MC_DTYPE_FP8_E4M3 = 3  /* OCP e4m3fn (gfx950 native fp8); contrastive GEMM operands only */
 } mc_dtype;
 
 enum {

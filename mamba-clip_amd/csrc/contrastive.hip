@@ -11,8 +11,12 @@
 //    through LDS in 64-byte row slices (80-byte padded rows: conflict-free
 //    fragment reads), next slice prefetched into registers under the MFMAs.
 //    bf16 inputs use v_mfma_f32_16x16x32_bf16 (fp32 accumulate); fp32 inputs
-//    use the exact-fp32 v_mfma_f32_16x16x4_f32.  alpha may live on the device
-//    (logit_scale.exp()), so the loss needs no host sync.
+//    use the exact-fp32 v_mfma_f32_16x16x4_f32, fp8 (OCP e4m3fn) inputs
+//    v_mfma_f32_16x16x32_fp8_fp8 with a 64-element K slice (two MFMA k-steps
+//    per LDS fragment read) and per-row dequantisation factors applied in the
+//    epilogue.  alpha may live on the device (logit_scale.exp()), so the loss
+//    needs no host sync.
+//  * quant_rows_fp8: one wave per row, amax -> 448/amax scale -> v_cvt_pk_fp8_f32.
 //  * ce_rows / ce_cols(+finalize): log-sum-exp statistics and per-label NLL
 //    along rows or columns, online max/sum, deterministic fixed-order
 //    partial reductions (no atomics).
@@ -39,8 +43,12 @@ struct GemmArgs {
   const void* B; int64_t ldb;
   void* C; int64_t ldc;
   float alpha; const float* alpha_dev;
+  const float* sa; const float* sb;   // per-row dequantisation (fp8), nullable
   int tiles_m, tiles_n;
+  int c_vec;                           // C 16-B aligned and ldc % 4 == 0: vector stores in full tiles
 };
+
+typedef uint8_t fp8_t;   // OCP e4m3fn bits
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
@@ -71,7 +79,10 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
       const int r = v >> 2, c = v & 3;
       const int kk = k0 + c * V;
       const int am = m0 + r, bn = n0 + r;
-      if (kAligned && kk + V <= g.K) {
+      if constexpr (E == 1) {   // fp8: K % 16 == 0 and 16-B rows (host-checked)
+        ra[i] = (am < g.M && kk < g.K) ? ld16(A + (int64_t)am * g.lda + kk) : make_uint4(0u, 0u, 0u, 0u);
+        rb[i] = (bn < g.N && kk < g.K) ? ld16(B + (int64_t)bn * g.ldb + kk) : make_uint4(0u, 0u, 0u, 0u);
+      } else if (kAligned && kk + V <= g.K) {
         ra[i] = am < g.M ? ld16(A + (int64_t)am * g.lda + kk) : make_uint4(0u, 0u, 0u, 0u);
         rb[i] = bn < g.N ? ld16(B + (int64_t)bn * g.ldb + kk) : make_uint4(0u, 0u, 0u, 0u);
       } else {
@@ -120,6 +131,27 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    } else if constexpr (E == 1) {
+      // fp8: lane reads 16 bytes = k 16*(l>>4) .. +15 of the 64-wide slice and feeds
+      // bytes 0-7 to k-step 0 and 8-15 to k-step 1.  A and B use the same lane -> k
+      // map, so each k of the slice is paired once (the sum is order-free in k).
+      uint4 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *reinterpret_cast<const uint4*>(la + (wr * 64 + i * 16 + (lane & 15)) * kLdsStride + (lane >> 4) * 16);
+        bf[i] = *reinterpret_cast<const uint4*>(lb + (wc * 64 + i * 16 + (lane & 15)) * kLdsStride + (lane >> 4) * 16);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const long a8 = h ? (long)(((uint64_t)af[i].w << 32) | af[i].z) : (long)(((uint64_t)af[i].y << 32) | af[i].x);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const long b8 = h ? (long)(((uint64_t)bf[j].w << 32) | bf[j].z) : (long)(((uint64_t)bf[j].y << 32) | bf[j].x);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b8, acc[i][j], 0, 0, 0);
+          }
+        }
     } else {
       // exact fp32: 4 MFMA K-steps of 4; lane holds A[row l&15][k = 4s + (l>>4)]
 #pragma unroll
@@ -145,18 +177,61 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
 
   const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
   TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
-  // C/D map of 16x16 MFMA: col = lane & 15, row = 4*(lane >> 4) + r
+  // Epilogue through LDS.  The 16x16 MFMA C/D map (col = lane & 15, row =
+  // 4*(lane >> 4) + r) would make every store instruction write 64-B pieces of
+  // four rows; instead each wave stages 32 x 64 of its results at a time
+  // (68-float padded rows: conflict-free both ways) and writes them back as
+  // 16-B vectors, 16 lanes per 256-B row segment (the two column waves of a
+  // tile complete each 512-B row).  For the N x N logits (C5: 268 MB fp32)
+  // this store stream is the kernel's HBM side.
+  constexpr int kEpStride = 68;
+  __syncthreads();                                          // main-loop LDS reads done
+  float* ep = reinterpret_cast<float*>(lds) + w * (32 * kEpStride);
+  const bool full = g.c_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int p = 0; p < 2; ++p) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * 64 + j * 16 + (lane & 15);
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int i = 2 * p + i2;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (row < g.M && col < g.N) C[(int64_t)row * g.ldc + col] = from_f<TOut>(alpha * acc[i][j][r]);
+      for (int j = 0; j < 4; ++j) {
+        const int col_l = j * 16 + (lane & 15);
+        const int col = n0 + wc * 64 + col_l;
+        const float cs = (g.sb && col < g.N) ? alpha * g.sb[col] : alpha;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row_l = i2 * 16 + 4 * (lane >> 4) + r;
+          const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+          const float sa = (g.sa && row < g.M) ? g.sa[row] : 1.f;
+          ep[row_l * kEpStride + col_l] = g.sa ? (acc[i][j][r] * sa) * cs : acc[i][j][r] * cs;
+        }
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int q = lane + 64 * t;
+      const int row_l = q >> 4, c4 = (q & 15) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c4);
+      const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c4;
+      TOut* dst = C + (int64_t)row * g.ldc + col;
+      if (full) {
+        if constexpr (sizeof(TOut) == 4) {
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));   // streamed: nothing re-reads it here
+        } else {
+          const uint32_t lo = bits16<TOut>(v[0]) | (bits16<TOut>(v[1]) << 16);
+          const uint32_t hi = bits16<TOut>(v[2]) | (bits16<TOut>(v[3]) << 16);
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(u32x2{lo, hi}, reinterpret_cast<u32x2*>(dst));
+        }
+      } else if (row < g.M) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col + e < g.N) dst[e] = from_f<TOut>(v[e]);
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------ CE statistics
@@ -299,6 +374,39 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(int rows, int cols, const 
   if (threadIdx.x == 0 && partial) partial[blockIdx.x] = red[0];
 }
 
+// ------------------------------------------------------------------ fp8 quantiser
+constexpr float kFp8Max = 448.f;   // e4m3fn max finite
+
+template <typename TIn>
+__global__ __launch_bounds__(256) void quant_rows_fp8_kernel(int rows, int cols, const TIn* __restrict__ X,
+                                                             int64_t ldx, fp8_t* __restrict__ Q, int64_t ldq,
+                                                             float* __restrict__ inv_scale) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + w;
+  if (row >= rows) return;
+  const TIn* xr = X + (int64_t)row * ldx;
+  float amax = 0.f;
+  for (int j = lane; j < cols; j += 64) amax = fmaxf(amax, fabsf(to_f(xr[j])));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  const float s = amax > 0.f ? kFp8Max / amax : 1.f;
+  if (lane == 0) inv_scale[row] = 1.f / s;
+  // each lane packs 4 consecutive bytes (one dword store) per step
+  uint32_t* qr = reinterpret_cast<uint32_t*>(Q + (int64_t)row * ldq);
+  const int nw = (int)(ldq >> 2);
+  for (int q = lane; q < nw; q += 64) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * q + e;
+      v[e] = j < cols ? fminf(fmaxf(to_f(xr[j]) * s, -kFp8Max), kFp8Max) : 0.f;
+    }
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], pk, true);
+    qr[q] = (uint32_t)pk;
+  }
+}
+
 constexpr int kColSplits = 32;
 constexpr int kGradGrid = 2048;
 
@@ -311,8 +419,8 @@ using namespace mc::ctr;
 extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_gemm_nt: null params");
   MC_CHECK(p->M >= 0 && p->N >= 0 && p->K >= 0, MC_ERR_SHAPE, "mc_gemm_nt: negative shape");
-  MC_CHECK(p->in_dtype == MC_DTYPE_BF16 || p->in_dtype == MC_DTYPE_F32, MC_ERR_DTYPE,
-           "mc_gemm_nt: inputs must be bf16 or fp32");
+  MC_CHECK(p->in_dtype == MC_DTYPE_BF16 || p->in_dtype == MC_DTYPE_F32 || p->in_dtype == MC_DTYPE_FP8_E4M3,
+           MC_ERR_DTYPE, "mc_gemm_nt: inputs must be bf16, fp32 or fp8 e4m3");
   MC_CHECK(p->out_dtype == MC_DTYPE_F32 || p->out_dtype == MC_DTYPE_BF16, MC_ERR_DTYPE,
            "mc_gemm_nt: output must be fp32 or bf16");
   if (p->M == 0 || p->N == 0) return MC_OK;
@@ -321,11 +429,16 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   g.M = p->M; g.N = p->N; g.K = p->K;
   g.A = p->A; g.lda = p->lda; g.B = p->B; g.ldb = p->ldb; g.C = p->C; g.ldc = p->ldc;
   g.alpha = p->alpha; g.alpha_dev = p->alpha_dev;
+  g.sa = p->row_scale_a; g.sb = p->row_scale_b;
+  g.c_vec = aligned16(p->C) && p->ldc % 4 == 0;
   g.tiles_m = (p->M + BM - 1) / BM;
   g.tiles_n = (p->N + BN - 1) / BN;
-  const int eb = p->in_dtype == MC_DTYPE_F32 ? 4 : 2;
+  const int eb = p->in_dtype == MC_DTYPE_F32 ? 4 : (p->in_dtype == MC_DTYPE_FP8_E4M3 ? 1 : 2);
   const int64_t v = 16 / eb;
   const bool aligned = aligned16(p->A) && aligned16(p->B) && p->lda % v == 0 && p->ldb % v == 0;
+  if (eb == 1)
+    MC_CHECK(aligned && p->K % 16 == 0, MC_ERR_SHAPE,
+             "mc_gemm_nt: fp8 operands need K, lda, ldb multiples of 16 and 16-B aligned rows");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(g.tiles_m * g.tiles_n), block(256);
 #define MC_GEMM(TI, TO)                                                                   \
@@ -335,6 +448,8 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   } while (0)
   if (p->in_dtype == MC_DTYPE_BF16) {
     if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(bf16_t, float); else MC_GEMM(bf16_t, bf16_t);
+  } else if (p->in_dtype == MC_DTYPE_FP8_E4M3) {
+    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(fp8_t, float); else MC_GEMM(fp8_t, bf16_t);
   } else {
     if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(float, float); else MC_GEMM(float, bf16_t);
   }
@@ -409,5 +524,31 @@ extern "C" int mc_ce_grad(int32_t rows, int32_t cols, const float* S, int64_t ld
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, grid, 1.f, scale_dev, dscale_out);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_ce_grad: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+extern "C" int mc_quant_rows_fp8(int32_t rows, int32_t cols, int32_t in_dtype, const void* X, int64_t ldx, uint8_t* Q,
+                                 int64_t ldq, float* inv_scale, void* stream) {
+  MC_CHECK(rows >= 0 && cols >= 0, MC_ERR_SHAPE, "mc_quant_rows_fp8: negative shape");
+  MC_CHECK(ldq % 16 == 0 && ldq >= cols, MC_ERR_SHAPE, "mc_quant_rows_fp8: ldq must be a multiple of 16 and >= cols");
+  MC_CHECK(ldx >= cols, MC_ERR_SHAPE, "mc_quant_rows_fp8: ldx < cols");
+  if (rows == 0) return MC_OK;
+  MC_CHECK(X && Q && inv_scale, MC_ERR_INVALID, "mc_quant_rows_fp8: null pointer");
+  MC_CHECK(aligned16(Q), MC_ERR_INVALID, "mc_quant_rows_fp8: Q must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((rows + 3) / 4), block(256);
+  if (in_dtype == MC_DTYPE_F32)
+    hipLaunchKernelGGL((quant_rows_fp8_kernel<float>), grid, block, 0, s, rows, cols,
+                       reinterpret_cast<const float*>(X), ldx, Q, ldq, inv_scale);
+  else if (in_dtype == MC_DTYPE_BF16)
+    hipLaunchKernelGGL((quant_rows_fp8_kernel<bf16_t>), grid, block, 0, s, rows, cols,
+                       reinterpret_cast<const bf16_t*>(X), ldx, Q, ldq, inv_scale);
+  else if (in_dtype == MC_DTYPE_F16)
+    hipLaunchKernelGGL((quant_rows_fp8_kernel<f16_t>), grid, block, 0, s, rows, cols,
+                       reinterpret_cast<const f16_t*>(X), ldx, Q, ldq, inv_scale);
+  else
+    MC_CHECK(false, MC_ERR_DTYPE, "mc_quant_rows_fp8: input must be fp32, bf16 or f16");
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_quant_rows_fp8: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }

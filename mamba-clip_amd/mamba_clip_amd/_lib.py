@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MAMBA_CLIP_AMD_LIB overrides the path (dev A/B builds only)
 LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB", os.path.join(_HERE, "libmamba_clip_amd.so"))
 
-MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16 = 0, 1, 2
+MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3 = 0, 1, 2, 3
 MC_SCAN_CHUNK = 8
 MC_SCAN_MAX_DSTATE = 32
 
@@ -66,6 +66,7 @@ class GemmNTParams(ctypes.Structure):
         ("M", c_i32), ("N", c_i32), ("K", c_i32), ("in_dtype", c_i32), ("out_dtype", c_i32),
         ("A", c_vp), ("lda", c_i64), ("B", c_vp), ("ldb", c_i64), ("C", c_vp), ("ldc", c_i64),
         ("alpha", ctypes.c_float), ("alpha_dev", c_fp),
+        ("row_scale_a", c_fp), ("row_scale_b", c_fp),
     ]
 
 
@@ -80,6 +81,7 @@ SYMBOLS = {
     "mc_scan_fwd": (ctypes.c_int, [ctypes.POINTER(ScanFwdParams), c_vp]),
     "mc_scan_bwd": (ctypes.c_int, [ctypes.POINTER(ScanBwdParams), c_vp]),
     "mc_gemm_nt": (ctypes.c_int, [ctypes.POINTER(GemmNTParams), c_vp]),
+    "mc_quant_rows_fp8": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_fp, c_vp]),
     "mc_ce_stats": (ctypes.c_int, [c_i32, c_i32, c_fp, c_i64, c_i32, c_i64, c_fp, c_fp, ctypes.c_float, c_fp,
                                    c_vp, ctypes.c_size_t, c_vp]),
     "mc_ce_stats_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
@@ -135,9 +137,10 @@ def check(rc, what):
 
 def dtype_code(dt):
     import torch
-    codes = {torch.float32: MC_DTYPE_F32, torch.bfloat16: MC_DTYPE_BF16, torch.float16: MC_DTYPE_F16}
+    codes = {torch.float32: MC_DTYPE_F32, torch.bfloat16: MC_DTYPE_BF16, torch.float16: MC_DTYPE_F16,
+             torch.float8_e4m3fn: MC_DTYPE_FP8_E4M3}
     if dt not in codes:
-        raise RuntimeError(f"mamba_clip_amd: unsupported dtype {dt} (float32, bfloat16, float16 only)")
+        raise RuntimeError(f"mamba_clip_amd: unsupported dtype {dt} (float32, bfloat16, float16, float8_e4m3fn only)")
     return codes[dt]
 
 

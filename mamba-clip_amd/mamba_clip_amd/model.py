@@ -340,12 +340,21 @@ class ClipModel(nn.Module):
             if hasattr(t, "set_grad_checkpointing"):
                 t.set_grad_checkpointing(enable)
 
-    def get_logits(self, image, text):
-        from .ops import gemm_nt
+    def get_logits(self, image, text, precision=None):
+        """(logits_per_image, logits_per_text) = scale * I @ T.T (model.py:1104-1112).
+
+        precision="fp8": the similarity matmul runs on the fp8 MFMA path with
+        row-wise e4m3fn quantisation of the normalised features (config 5).
+        """
+        from .ops import gemm_nt, similarity_fp8
         i = self.encode_image(image, normalize=True)
         t = self.encode_text(text, normalize=True)
-        dt = i.dtype if i.dtype == torch.bfloat16 else torch.float32
-        image_logits = gemm_nt(i.to(dt), t.to(dt), alpha_dev=self.logit_scale.exp().float().reshape(()))
+        scale = self.logit_scale.exp().float().reshape(())
+        if precision == "fp8":
+            image_logits = similarity_fp8(i, t, scale)
+        else:
+            dt = i.dtype if i.dtype == torch.bfloat16 else torch.float32
+            image_logits = gemm_nt(i.to(dt), t.to(dt), alpha_dev=scale)
         if self.logit_bias is not None:
             image_logits = image_logits + self.logit_bias
         return image_logits, image_logits.T

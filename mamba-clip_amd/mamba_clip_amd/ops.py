@@ -1,6 +1,8 @@
 """Thin torch-facing wrappers of the contrastive kernels (include/mc_contrastive.h).
 
-``gemm_nt(A, B, alpha)``  C = alpha * A @ B.T on the matrix cores (bf16 or fp32 in).
+``gemm_nt(A, B, alpha)``  C = alpha * A @ B.T on the matrix cores (bf16, fp32 or fp8 e4m3fn in).
+``quant_rows_fp8(X)``     row-wise amax-scaled e4m3fn quantisation (K padded to 16).
+``similarity_fp8(I, T, scale)``  scale * I @ T.T through the fp8 MFMA path (config 5).
 ``scaled_logits_ce``      autograd op: logits = scale * X @ Y.T, then a weighted
                           sum of row- and/or column-softmax cross-entropies --
                           the dense part of ClipLoss (loss.py:89-147).
@@ -15,11 +17,15 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
-def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32):
-    """C[m, n] = alpha * sum_k A[m, k] * B[n, k]  (A, B row-major, K contiguous)."""
+def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32, scale_a=None, scale_b=None):
+    """C[m, n] = alpha * scale_a[m] * scale_b[n] * sum_k A[m, k] * B[n, k]  (A, B row-major, K contiguous).
+
+    scale_a / scale_b (fp32 per-row factors, optional) are the dequantisation
+    factors of fp8 operands from ``quant_rows_fp8``.
+    """
     lib = _lib.load()
-    if A.dtype != B.dtype or A.dtype not in (torch.bfloat16, torch.float32):
-        raise RuntimeError("gemm_nt: A and B must both be bf16 or both fp32")
+    if A.dtype != B.dtype or A.dtype not in (torch.bfloat16, torch.float32, torch.float8_e4m3fn):
+        raise RuntimeError("gemm_nt: A and B must both be bf16, both fp32 or both float8_e4m3fn")
     if A.stride(-1) != 1:
         A = A.contiguous()
     if B.stride(-1) != 1:
@@ -35,8 +41,50 @@ def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32):
     p.A, p.lda, p.B, p.ldb, p.C, p.ldc = A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), N
     p.alpha = float(alpha)
     p.alpha_dev = alpha_dev.data_ptr() if alpha_dev is not None else None
+    for name, sc, n in (("row_scale_a", scale_a, M), ("row_scale_b", scale_b, N)):
+        if sc is not None:
+            if sc.dtype != torch.float32 or sc.numel() != n or not sc.is_contiguous():
+                raise RuntimeError(f"gemm_nt: {name} must be a contiguous fp32 vector of {n} entries")
+            setattr(p, name, sc.data_ptr())
     _lib.check(lib.mc_gemm_nt(p, _lib.stream_handle(A.device)), "mc_gemm_nt")
     return C
+
+
+def quant_rows_fp8(X):
+    """(Q, inv_scale): Q (rows, round_up(cols, 16)) float8_e4m3fn, zero-padded; X[i] ~= Q[i] * inv_scale[i].
+
+    Row scale s_i = 448 / max_j |X[i, j]| (include/mc_contrastive.h, mc_quant_rows_fp8).
+    """
+    lib = _lib.load()
+    if not X.is_cuda:
+        raise RuntimeError("quant_rows_fp8: X must be a HIP (cuda) tensor")
+    if X.dim() != 2:
+        raise RuntimeError("quant_rows_fp8: X must be 2-D")
+    if X.stride(-1) != 1:
+        X = X.contiguous()
+    rows, cols = X.shape
+    ldq = (cols + 15) // 16 * 16
+    Q = torch.empty(rows, ldq, device=X.device, dtype=torch.float8_e4m3fn)
+    inv = torch.empty(rows, device=X.device, dtype=torch.float32)
+    _lib.check(lib.mc_quant_rows_fp8(rows, cols, _lib.dtype_code(X.dtype), X.data_ptr(), X.stride(0) if rows else cols,
+                                     Q.data_ptr(), ldq, inv.data_ptr(), _lib.stream_handle(X.device)),
+               "mc_quant_rows_fp8")
+    return Q, inv
+
+
+def similarity_fp8(image_features, text_features, logit_scale, out_dtype=torch.float32):
+    """logit_scale * I @ T.T with both operands quantised row-wise to e4m3fn (fp32 accumulate).
+
+    The similarity matmul of ClipModel.get_logits (model.py:1104-1112) on
+    frozen features, fp8 MFMA (BASELINE config 5).  ``logit_scale`` is the
+    already-exponentiated scale (a 0-d device tensor or a float).
+    """
+    qi, si = quant_rows_fp8(image_features)
+    qt, st = quant_rows_fp8(text_features)
+    if torch.is_tensor(logit_scale):
+        return gemm_nt(qi, qt, alpha_dev=logit_scale.reshape(()).float().contiguous(), out_dtype=out_dtype,
+                       scale_a=si, scale_b=st)
+    return gemm_nt(qi, qt, alpha=float(logit_scale), out_dtype=out_dtype, scale_a=si, scale_b=st)
 
 
 def ce_stats(S, axis, label_offset, coef):

@@ -69,3 +69,21 @@ def test_loss_oracle_single_process(fname):
     torch.testing.assert_close(img.grad, g["grad_img"], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(txt.grad, g["grad_txt"], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(s.grad.reshape(1), g["grad_scale"], rtol=1e-5, atol=1e-7)
+
+
+def test_quant_rows_fp8_ref_properties():
+    """fp8 oracle (config 5): padding, zero rows, scale and the e4m3 round-trip bound."""
+    from oracle.loss_ref import quant_rows_fp8_ref, similarity_fp8_ref
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(9, 40, generator=g) * 5
+    X[3] = 0
+    q, inv = quant_rows_fp8_ref(X)
+    assert q.shape == (9, 48) and q.dtype == torch.uint8
+    assert (q[:, 40:] == 0).all() and (q[3] == 0).all() and inv[3] == 1.0
+    deq = q[:, :40].view(torch.float8_e4m3fn).float() * inv[:, None]
+    assert ((deq - X).abs() <= X.abs() * 2 ** -4 + inv[:, None] * 2 ** -9).all()
+    # every nonzero row uses the full range: its largest element maps to 448 exactly
+    full = q[:, :40].view(torch.float8_e4m3fn).float().abs().amax(dim=1)
+    assert torch.equal(full[torch.arange(9) != 3], torch.full((8,), 448.0))
+    S = similarity_fp8_ref(X, X, 1.0)
+    assert torch.allclose(S, S.T)
