@@ -46,6 +46,7 @@ struct GemmArgs {
   const float* sa; const float* sb;   // per-row dequantisation (fp8), nullable
   int tiles_m, tiles_n;
   int c_vec;                           // C 16-B aligned and ldc % 4 == 0: vector stores in full tiles
+  int c_vec16;                         // 16-bit C: ldc % 8 == 0 as well (16-B stores of 8 values)
 };
 
 typedef uint8_t fp8_t;   // OCP e4m3fn bits
@@ -64,8 +65,17 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
+  // Each XCD gets a contiguous range of tile ids (xcd_remap); inside it, tiles
+  // go in groups of kGroupM tile rows swept column by column, so the
+  // workgroups resident on one XCD at a time share ~8 A row blocks and a
+  // dozen B column blocks in that XCD's 4 MB L2 instead of streaming all of B
+  // (C5: 8192 x 512 fp8 = 4 MB per operand, each block read 64 times).
+  constexpr int kGroupM = 8;
   const int bid = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
-  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int first_m = (bid / (kGroupM * g.tiles_n)) * kGroupM;
+  const int gm = min(g.tiles_m - first_m, kGroupM);
+  const int local = bid % (kGroupM * g.tiles_n);
+  const int tm = first_m + local % gm, tn = local / gm;
   const int m0 = tm * BM, n0 = tn * BN;
   const TIn* __restrict__ A = reinterpret_cast<const TIn*>(g.A);
   const TIn* __restrict__ B = reinterpret_cast<const TIn*>(g.B);
@@ -208,26 +218,42 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
       }
     }
     __syncthreads();
+    if constexpr (sizeof(TOut) == 4) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int q = lane + 64 * t;
-      const int row_l = q >> 4, c4 = (q & 15) * 4;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c4);
-      const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c4;
-      TOut* dst = C + (int64_t)row * g.ldc + col;
-      if (full) {
-        if constexpr (sizeof(TOut) == 4) {
+      for (int t = 0; t < 8; ++t) {      // 4 floats per lane, 16 lanes per row segment
+        const int q = lane + 64 * t;
+        const int row_l = q >> 4, c4 = (q & 15) * 4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c4);
+        const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c4;
+        TOut* dst = C + (int64_t)row * g.ldc + col;
+        if (full) {
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));   // streamed: nothing re-reads it here
-        } else {
-          const uint32_t lo = bits16<TOut>(v[0]) | (bits16<TOut>(v[1]) << 16);
-          const uint32_t hi = bits16<TOut>(v[2]) | (bits16<TOut>(v[3]) << 16);
-          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-          __builtin_nontemporal_store(u32x2{lo, hi}, reinterpret_cast<u32x2*>(dst));
-        }
-      } else if (row < g.M) {
+        } else if (row < g.M) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (col + e < g.N) dst[e] = from_f<TOut>(v[e]);
+          for (int e = 0; e < 4; ++e)
+            if (col + e < g.N) dst[e] = from_f<TOut>(v[e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {      // 8 values -> one 16-B store per lane, 8 lanes per row segment
+        const int q = lane + 64 * t;
+        const int row_l = q >> 3, c8 = (q & 7) * 8;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c8 + 4);
+        const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c8;
+        TOut* dst = C + (int64_t)row * g.ldc + col;
+        if (full && g.c_vec16) {
+          const u32x4_t pk = {bits16<TOut>(v0[0]) | (bits16<TOut>(v0[1]) << 16),
+                              bits16<TOut>(v0[2]) | (bits16<TOut>(v0[3]) << 16),
+                              bits16<TOut>(v1[0]) | (bits16<TOut>(v1[1]) << 16),
+                              bits16<TOut>(v1[2]) | (bits16<TOut>(v1[3]) << 16)};
+          __builtin_nontemporal_store(pk, reinterpret_cast<u32x4_t*>(dst));
+        } else if (row < g.M) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (col + e < g.N) dst[e] = from_f<TOut>(e < 4 ? v0[e] : v1[e - 4]);
+        }
       }
     }
     __syncthreads();
@@ -431,6 +457,7 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   g.alpha = p->alpha; g.alpha_dev = p->alpha_dev;
   g.sa = p->row_scale_a; g.sb = p->row_scale_b;
   g.c_vec = aligned16(p->C) && p->ldc % 4 == 0;
+  g.c_vec16 = g.c_vec && p->ldc % 8 == 0;
   g.tiles_m = (p->M + BM - 1) / BM;
   g.tiles_n = (p->N + BN - 1) / BN;
   const int eb = p->in_dtype == MC_DTYPE_F32 ? 4 : (p->in_dtype == MC_DTYPE_FP8_E4M3 ? 1 : 2);
