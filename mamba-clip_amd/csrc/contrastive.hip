@@ -114,6 +114,23 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
     }
   };
 
+  // epilogue scale factors loaded up front: their latency hides under the K loop
+  // instead of sitting in the epilogue's dependency chain
+  const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
+  float col_scale[4], row_scale[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wc * 64 + j * 16 + (lane & 15);
+    col_scale[j] = (g.sb && col < g.N) ? g.sb[col] : 1.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+      row_scale[i][r] = (g.sa && row < g.M) ? g.sa[row] : 1.f;
+    }
+
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -185,7 +202,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
     }
   }
 
-  const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
   TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
   // Epilogue through LDS.  The 16x16 MFMA C/D map (col = lane & 15, row =
   // 4*(lane >> 4) + r) would make every store instruction write 64-B pieces of
@@ -206,14 +222,11 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col_l = j * 16 + (lane & 15);
-        const int col = n0 + wc * 64 + col_l;
-        const float cs = (g.sb && col < g.N) ? alpha * g.sb[col] : alpha;
+        const float cs = alpha * col_scale[j];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row_l = i2 * 16 + 4 * (lane >> 4) + r;
-          const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
-          const float sa = (g.sa && row < g.M) ? g.sa[row] : 1.f;
-          ep[row_l * kEpStride + col_l] = g.sa ? (acc[i][j][r] * sa) * cs : acc[i][j][r] * cs;
+          ep[row_l * kEpStride + col_l] = (acc[i][j][r] * row_scale[i][r]) * cs;
         }
       }
     }
