@@ -44,8 +44,8 @@ C2_FLOP_PER_PAIR = 146e9         # fwd+bwd, SURVEY.md 8(d)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="pairs per GPU")
     ap.add_argument("--model", default="vit_b16-mamba130m")
     ap.add_argument("--scan-iters", type=int, default=20)
@@ -109,7 +109,8 @@ def scan_roofline(iters, warmup=3):
     return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
-            "traffic_source": traffic_src, "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+            "traffic_source": traffic_src, "traffic_measured_in_this_run": False,
+            "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
 
 
 def similarity_c5(iters=20, warmup=3):
@@ -183,6 +184,20 @@ def cpu_baseline(args, model_name):
                       f"{args.cpu_batch} via oracle/cpu_model.py ({secs:.1f} s timed)"}
 
 
+def cpu_baseline_scan(args):
+    """The scan half of the metric on the host: the oracle's restatement of the reference semantics
+    (model.py:83-169) on one C4 sequence batch (B=1 of 64, D=3072, L=4096, N=16, bf16 I/O)."""
+    import torch
+    from oracle.cpu_model import cpu_scan_gbps
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    gbs, secs = cpu_scan_gbps(batch=1, dim=3072, seqlen=4096, dstate=16, threads=threads)
+    torch.set_num_threads(prev)
+    return {"value": round(gbs, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"selective_scan fwd, oracle/scan_ref.py (reference semantics), B=1 x D=3072 x L=4096 x N=16 "
+                      f"bf16 I/O, algorithmic bytes as the roofline ({secs:.1f} s)"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -226,9 +241,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    stream = torch.cuda.current_stream(device)
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks[0].record(stream)
+    for k in range(args.steps):
         losses = step()
+        marks[k + 1].record(stream)          # per-step HIP events: no host sync inside the timed loop
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -242,11 +261,16 @@ def main():
     if not math.isfinite(final_loss):
         raise RuntimeError(f"non-finite training loss {final_loss}")
 
+    step_ms = sorted(marks[k].elapsed_time(marks[k + 1]) for k in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1]
+                                                                             + step_ms[len(step_ms) // 2])
     value = world * args.batch * args.steps / elapsed
     result = {
         "metric": "image-text pairs/sec (whole node) + selective_scan HBM GB/s",
         "value": round(value, 2), "unit": "image-text pairs/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "median_ms_per_step": round(median_ms, 3),
+        "median_pairs_per_sec": round(world * args.batch / (median_ms * 1e-3), 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) 77-token text, EOT last)",
         "config": {"workload": "C2: ViT-B/16 image + Mamba-130M text, contrastive train step "
@@ -269,6 +293,7 @@ def main():
         result["similarity_fp8"] = similarity_c5()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.model)
+        result["cpu_baseline_scan"] = cpu_baseline_scan(args)
     if world > 1:
         dist.barrier()
     if rank == 0:

@@ -135,7 +135,8 @@ def main(argv=None):
     img_size = getattr(inner.visual, "patch_embed", None)
     img_size = img_size.grid * img_size.patch if img_size is not None else 224
     data = get_synthetic_data(args.batch_size, n_batches, img_size, text.context_length, text.vocab_size, device,
-                              seed=1000 + args.rank)
+                              seed=1000 + args.rank, balanced=args.balanced_mixup is not None,
+                              num_classes=args.num_classes)
     total_steps = n_batches // args.accum_freq * args.epochs
     scheduler = _make_scheduler(optimizer, args, total_steps)
 

@@ -21,8 +21,12 @@ def synthetic_batch(batch, image_size, context_length, vocab_size, num_classes=2
 
 
 class _SyntheticLoader:
-    def __init__(self, batch, num_batches, **kw):
-        self.batch, self.num_batches, self.kw = batch, num_batches, kw
+    """Yields the same device-resident batch num_batches times; with balanced=True
+    the ComboLoader pair (batch, balanced batch) that --balanced-mixup consumes
+    (reference data.py:218-239, train.py:131-151)."""
+
+    def __init__(self, batch, num_batches, balanced=False, **kw):
+        self.batch, self.num_batches, self.kw, self.balanced = batch, num_batches, kw, balanced
         self.num_samples = batch * num_batches
         self._cached = None
 
@@ -31,7 +35,10 @@ class _SyntheticLoader:
 
     def __iter__(self):
         if self._cached is None:
-            self._cached = synthetic_batch(self.batch, **self.kw)
+            b = synthetic_batch(self.batch, **self.kw)
+            if self.balanced:
+                b = (b, synthetic_batch(self.batch, **dict(self.kw, seed=self.kw.get("seed", 0) + 7919)))
+            self._cached = b
         for _ in range(self.num_batches):
             yield self._cached
 
@@ -48,7 +55,8 @@ class DataInfo:
 
 
 def get_synthetic_data(batch, num_batches, image_size, context_length, vocab_size, device, seed=0,
-                       image_dtype=torch.float32):
-    loader = _SyntheticLoader(batch, num_batches, image_size=image_size, context_length=context_length,
-                              vocab_size=vocab_size, device=device, seed=seed, image_dtype=image_dtype)
+                       image_dtype=torch.float32, balanced=False, num_classes=2):
+    loader = _SyntheticLoader(batch, num_batches, balanced=balanced, image_size=image_size,
+                              context_length=context_length, vocab_size=vocab_size, num_classes=num_classes,
+                              device=device, seed=seed, image_dtype=image_dtype)
     return {"train": DataInfo(loader)}

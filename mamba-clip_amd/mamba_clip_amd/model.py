@@ -128,7 +128,12 @@ class MambaTextEncoder(nn.Module):
         self.norm_f = nn.Parameter(torch.ones(d_model))
         self.proj = nn.Linear(d_model, output_dim, bias=False)
         nn.init.normal_(self.proj.weight, std=d_model ** -0.5)
-        self.transformer = self.layers  # lock_text_tower walks .transformer (model.py:1072-1097)
+
+    def lock_units(self):
+        """(embeddings, [layer, ...], final norm) as lists of (name, parameter) for lock_text_tower."""
+        return ([("embedding.weight", self.embedding.weight)],
+                [list(l.named_parameters(prefix=f"layers.{i}")) for i, l in enumerate(self.layers)],
+                [("norm_f", self.norm_f)])
 
     def forward(self, tokens):
         Bsz, T = tokens.shape
@@ -275,7 +280,12 @@ class BertTextEncoder(nn.Module):
         self.blocks = nn.ModuleList([ViTBlock(width, heads) for _ in range(layers)])
         self.proj = nn.Sequential(nn.Linear(width, (width + output_dim) // 2, bias=False), nn.GELU(),
                                   nn.Linear((width + output_dim) // 2, output_dim, bias=False))
-        self.transformer = self.blocks
+
+    def lock_units(self):
+        """(embeddings incl. their LayerNorm, [block, ...], nothing after) for lock_text_tower."""
+        return ([("tok.weight", self.tok.weight), ("pos", self.pos), ("ln.weight", self.ln.weight),
+                 ("ln.bias", self.ln.bias)],
+                [list(b.named_parameters(prefix=f"blocks.{i}")) for i, b in enumerate(self.blocks)], [])
 
     def forward(self, tokens):
         m, h = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]]), None
@@ -285,18 +295,32 @@ class BertTextEncoder(nn.Module):
 
 
 # ============================================================================ CLIP wrapper (model.py:998-1112)
+def _is_norm_param(name):
+    """Our towers' LayerNorm / RMSNorm parameters (the HF towers' "LayerNorm" modules)."""
+    leaf = name.split(".")
+    return any(part in ("ln", "norm1", "norm2", "norm_weight", "norm_f") for part in leaf)
+
 class ClipModel(nn.Module):
+    """ClipModel(model) as the reference (model.py:1001-1009): wraps a CLIP-like model and SHARES its
+    visual / text towers and its logit_scale / logit_bias parameters.  ClipModel(visual, text) builds
+    one from two towers with fresh logit_scale = log(1/0.07) (and optional logit_bias)."""
     output_dict = True
 
-    def __init__(self, visual, text, init_logit_scale=math.log(1 / 0.07), init_logit_bias=None):
+    def __init__(self, model, text=None, init_logit_scale=math.log(1 / 0.07), init_logit_bias=None):
         super().__init__()
         self.output_dict = True
-        self.visual = visual
-        self.text = text
-        self.context_length = getattr(text, "context_length", None)
-        self.vocab_size = getattr(text, "vocab_size", None)
-        self.logit_scale = nn.Parameter(torch.ones([]) * init_logit_scale)
-        self.logit_bias = nn.Parameter(torch.ones([]) * init_logit_bias) if init_logit_bias is not None else None
+        if text is None:                      # reference form: a model with .visual / .text / .logit_scale
+            self.visual = model.visual
+            self.text = model.text
+            self.logit_scale = model.logit_scale
+            self.logit_bias = getattr(model, "logit_bias", None)
+        else:
+            self.visual = model
+            self.text = text
+            self.logit_scale = nn.Parameter(torch.ones([]) * init_logit_scale)
+            self.logit_bias = nn.Parameter(torch.ones([]) * init_logit_bias) if init_logit_bias is not None else None
+        self.context_length = getattr(self.text, "context_length", None)
+        self.vocab_size = getattr(self.text, "vocab_size", None)
 
     def encode_image(self, image, normalize: bool = False):
         f = self.visual(image)
@@ -329,11 +353,15 @@ class ClipModel(nn.Module):
         self.visual.lock(unlocked_groups=unlocked_groups, freeze_bn_stats=freeze_bn_stats)
 
     def lock_text_tower(self, unlocked_layers: int = 0, freeze_layer_norm: bool = True):
-        layers = list(getattr(self.text, "transformer", []))
-        frozen = layers if not unlocked_layers else layers[:-unlocked_layers]
-        for m in frozen:
-            for n, p in m.named_parameters():
-                p.requires_grad = (not freeze_layer_norm) and ("norm" in n.lower())
+        """model.py:1072-1097: freeze the text transformer -- embeddings, every layer (and the final
+        norm) -- or, with unlocked_layers = k, [embeddings, *layers][:-k]; norm parameters follow
+        `not freeze_layer_norm`.  The output projection stays trainable (it is not part of the
+        HF transformer the reference freezes)."""
+        emb, layers, final = self.text.lock_units()
+        units = [emb, *layers, final] if not unlocked_layers else [emb, *layers][:-unlocked_layers]
+        for unit in units:
+            for n, p in unit:
+                p.requires_grad = (not freeze_layer_norm) if _is_norm_param(n) else False
 
     def set_grad_checkpointing(self, enable=True):
         for t in (self.visual, self.text):
@@ -654,7 +682,7 @@ def init_model(model, tokenizer=None, aug_cfg=None, is_clip=False, use_tokenizer
     elif callable(model):
         model = model()
     if is_clip and not isinstance(model, ClipModel):
-        model = ClipModel(model.visual, model.text)
+        model = ClipModel(model)          # shares the towers AND logit_scale / logit_bias (model.py:1274-1275)
     if use_tokenizer and tokenizer is not None and callable(tokenizer):
         tokenizer = tokenizer()
     identity = (lambda x: x)

@@ -5,10 +5,17 @@ towers -> ClipLoss (HIP contrastive kernels, RCCL feature all-gather) ->
 backward (DDP bucketed RCCL all-reduce overlapped with the tail of backward)
 -> optional grad clip -> AdamW -> logit_scale.clamp_(0, ln 100).
 
+Batches are either (images, texts, targets) / (images, targets), or -- with
+--balanced-mixup -- the ComboLoader pair ((images, texts, targets),
+(bal_images, bal_texts, bal_targets)) as train.py:131-151 unpacks it.
+
 Differences from the reference are deliberate fixes:
-balanced-mixup variables are only touched when balanced mixup is on (A.2),
-and the accumulation path passes the concatenated features to the loss (the
-reference builds `inputs` and then ignores it).
+balanced-mixup variables are only touched when balanced mixup is on (A.1:
+the reference raises UnboundLocalError without it), and the accumulation path
+passes the concatenated features to the loss (the reference builds `inputs`
+and then ignores it).  Everything the reference computes is kept, including
+that get_model_inputs mixes the one-hot targets but returns only the model
+inputs, so the loss sees the original targets (train.py:66-89, 189).
 """
 import logging
 import math
@@ -136,12 +143,35 @@ def optimizer_step(model, optimizer, scaler, args):
             inner.logit_scale.clamp_(0, math.log(100))
 
 
-def train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast=None):
-    """One accum_freq == 1 step on device-resident inputs; returns the loss dict (device tensors)."""
+def split_batch(batch, balanced_mixup):
+    """train.py:131-157: -> (images, texts, targets, balanced) with balanced = (img, txt, tgt) or None."""
+    def unpack(b):
+        return (b[0], b[1], b[2]) if len(b) == 3 else (b[0], None, b[1])
+    if balanced_mixup:
+        return unpack(batch[0]) + (unpack(batch[1]),)
+    return unpack(batch) + (None,)
+
+
+def _balanced_to(balanced, device, input_dtype):
+    if balanced is None:
+        return None
+    img, txt, tgt = balanced
+    return (img.to(device=device, dtype=input_dtype), txt.to(device=device) if txt is not None else None,
+            tgt.to(device=device))
+
+
+def train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast=None, balanced=None):
+    """One accum_freq == 1 step on device-resident inputs; returns the loss dict (device tensors).
+
+    balanced: the balanced-mixup partner batch (images, texts, targets), required
+    when args.balanced_mixup is set (train.py:131-151, 169-177).
+    """
     autocast = autocast or get_autocast(args.precision)
+    if getattr(args, "balanced_mixup", None) and balanced is None:
+        raise ValueError("balanced_mixup needs the paired balanced batch ((img, txt, tgt), (bal_img, bal_txt, bal_tgt))")
     optimizer.zero_grad(set_to_none=True)
     with autocast():
-        model_out = model(*get_model_inputs(args, images, texts, targets))
+        model_out = model(*get_model_inputs(args, images, texts, targets, *(balanced or (None, None, None))))
         total, losses = _loss_terms(loss, model_out, targets)
     backward(total, scaler)
     optimizer_step(model, optimizer, scaler, args)
@@ -153,21 +183,30 @@ def train_step_accum(model, batches, loss, optimizer, scaler, args, autocast=Non
 
     Features of every micro-batch are computed without grad; then each micro-batch
     is re-run with grad and its loss uses the other micro-batches' cached
-    features as extra negatives.
+    features as extra negatives.  A batch is (images, texts, targets) or, with
+    balanced mixup, (images, texts, targets, balanced); the mixup is drawn in the
+    caching pass (the reference re-draws it in the re-run too, from stale
+    balanced tensors: train.py:249-257).
     """
     autocast = autocast or get_autocast(args.precision)
     cached = {}
+    mixed = []
     with torch.no_grad(), autocast():
-        for images, texts, targets in batches:
-            out = model(*get_model_inputs(args, images, texts, targets))
+        for batch in batches:
+            images, texts, targets = batch[:3]
+            bal = batch[3] if len(batch) > 3 else None
+            inp = get_model_inputs(args, images, texts, targets, *(bal or (None, None, None)))
+            mixed.append(inp)
+            out = model(*inp)
             for k, v in out.items():
                 if k not in ("logit_scale", "logit_bias"):
                     cached.setdefault(k, []).append(v)
     optimizer.zero_grad(set_to_none=True)
     losses = None
-    for j, (images, texts, targets) in enumerate(batches):
+    for j, batch in enumerate(batches):
+        targets = batch[2]
         with autocast():
-            out = model(*get_model_inputs(args, images, texts, targets))
+            out = model(*mixed[j])
             inputs = {k: out[k] for k in ("logit_scale", "logit_bias") if k in out}
             for k, vals in cached.items():
                 inputs[k] = torch.cat(vals[:j] + [out[k]] + vals[j + 1:])
@@ -195,15 +234,16 @@ def train_one_epoch(model, data, loss, epoch, optimizer, scaler, scheduler, args
         step = num_batches_per_epoch * epoch + i_accum
         if scheduler is not None and not getattr(args, "skip_scheduler", False):
             scheduler(step)
-        images, texts, targets = batch if len(batch) == 3 else (batch[0], None, batch[1])
+        images, texts, targets, balanced = split_batch(batch, getattr(args, "balanced_mixup", None))
+        balanced = _balanced_to(balanced, device, input_dtype)
         images = images.to(device=device, dtype=input_dtype, non_blocking=True)
         texts = texts.to(device=device, non_blocking=True) if texts is not None else None
         targets = targets.to(device=device, non_blocking=True)
         data_time_m.update(time.time() - end)
         if accum == 1:
-            losses = train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast)
+            losses = train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast, balanced)
         else:
-            pending.append((images, texts, targets))
+            pending.append((images, texts, targets, balanced))
             if (i + 1) % accum:
                 continue
             losses = train_step_accum(model, pending, loss, optimizer, scaler, args, autocast)

@@ -20,6 +20,18 @@ What it produces (small safetensors files next to this script):
   (model.py:297-723) imported with stub modules for the absent third-party
   packages (open_clip, timm, mamba_ssm); the scan inside is the executed
   reference text above.  State dict, input, output and input gradient.
+  ss2d_c1_d128_h16w16 is C1's exact shape; vssm_tiny_d16 a reduced VSSM
+  (model.py:868-995) end to end.
+* train_{clip,classifier}_mixup.safetensors -- the reference's own
+  pipeline.prepare_params (AdamW groups + cosine schedule, pipeline.py:205-408)
+  and train_one_epoch (train.py:92-385, balanced mixup on: the only way it
+  runs) for two epochs of a toy model
+  (tests/toy_models.py): per-step losses and lrs, initial and final weights,
+  the optimizer's group membership.
+* schedulers.safetensors -- scheduler.py's three schedules, with and without
+  restarts, at steps 0..39.
+
+Select generators on the command line (scan loss ss2d c1 train); none = all.
 """
 import ast
 import os
@@ -229,7 +241,7 @@ def import_reference_model(ref_scan):
         def __init__(self, *a, **k):
             raise RuntimeError("open_clip is not available offline")
     _stub("open_clip", CustomTextCLIP=_Dummy, create_model_from_pretrained=_Dummy,
-          get_tokenizer=_Dummy)
+          get_tokenizer=_Dummy, trace_model=_Dummy)
     _stub("open_clip.transform", PreprocessCfg=_Dummy)
     _stub("open_clip_train")
     _stub("open_clip_train.train", unwrap_model=lambda m: getattr(m, "module", m))
@@ -242,7 +254,8 @@ def import_reference_model(ref_scan):
     _stub("timm.layers")
     _stub("timm.layers.drop", DropPath=DropPath)
     sys.path.insert(0, REF_SRC)
-    _stub("mamba_clip.data", get_transform=lambda *a, **k: None)
+    _stub("mamba_clip.data", get_transform=lambda *a, **k: None, ComboLoader=_Dummy,
+          get_combo_loader=_Dummy, get_data=_Dummy, modify_loader=_Dummy)
     import importlib
     return importlib.import_module("mamba_clip.model")
 
@@ -272,8 +285,146 @@ def gen_ss2d(ref_scan):
     print("wrote ss_conv_ssm")
 
 
+def gen_c1(ref_scan):
+    """C1's exact SS2D shape (d_model=128 on 16x16, batch 8; BASELINE configs[0]) and a
+    reduced VSSM (every stage, PatchEmbed2D / PatchMerging2D / SS_Conv_SSM, a 1x1 last
+    stage) -- forward, input gradient and (SS2D) every parameter gradient.
+
+    The large inputs are NOT stored: they are regenerated from the seed by the test
+    (torch's CPU generator is deterministic for this torch version); a checksum of
+    them is stored so a mismatch fails loudly instead of silently comparing garbage."""
+    model = import_reference_model(ref_scan)
+    torch.manual_seed(2024)
+    m = model.SS2D(d_model=128).eval()
+    g = torch.Generator().manual_seed(2025)
+    x = torch.randn(8, 16, 16, 128, generator=g)
+    gy = torch.randn(8, 16, 16, 128, generator=g)
+    xg = x.clone().requires_grad_(True)
+    y = m(xg)
+    y.backward(gy)
+    tensors = {f"sd.{k}": v.detach().contiguous() for k, v in m.state_dict().items()}
+    tensors.update({f"grad.{k}": p.grad.detach().contiguous() for k, p in m.named_parameters()})
+    tensors.update({"y": y.detach(), "gx": xg.grad,
+                    "x_checksum": torch.stack([x.double().sum(), x.double().abs().sum(), gy.double().sum()])})
+    save_file(tensors, os.path.join(HERE, "ss2d_c1_d128_h16w16.safetensors"),
+              metadata={"d_model": "128", "x": "randn(8,16,16,128) then gy, Generator seed 2025"})
+    print("wrote ss2d c1", tuple(y.shape))
+
+    torch.manual_seed(45)
+    v = model.VSSM(patch_size=4, in_chans=3, num_classes=2, depths=[1, 1, 2, 1], dims=[16, 32, 64, 128],
+                   d_state=16).eval()
+    g = torch.Generator().manual_seed(46)
+    x = torch.randn(2, 3, 32, 32, generator=g).requires_grad_(True)
+    y = v(x)
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy)
+    tensors = {f"sd.{k}": t.detach().contiguous() for k, t in v.state_dict().items()}
+    tensors.update({"x": x.detach(), "y": y.detach(), "gy": gy, "gx": x.grad,
+                    "grad.head.weight": v.head.weight.grad})
+    save_file(tensors, os.path.join(HERE, "vssm_tiny_d16.safetensors"),
+              metadata={"depths": "1,1,2,1", "dims": "16,32,64,128", "img": "32"})
+    print("wrote vssm tiny", tuple(y.shape))
+
+
+# --------------------------------------------------------------------------
+# train step / optimizer groups / schedulers: the reference's train.py,
+# pipeline.prepare_params and scheduler.py, as-is, on toy models
+# --------------------------------------------------------------------------
+TRAIN_ARGS = dict(force_image_size=None, seed=0, rank=0, local_rank=0, siglip=False, use_bnb_linear=None,
+                  trace=False, lock_image=False, lock_text=False, grad_checkpointing=False, name="toy",
+                  distributed=False, wd=0.1, lr=1e-2, beta1=0.9, beta2=0.98, eps=1e-6, precision="fp32",
+                  resume=None, accum_freq=1, epochs=2, lr_restart_interval=None, warmup=1,
+                  lr_scheduler="cosine", tensorboard=False, hyperparameter_tuning=False, wandb=False,
+                  torchcompile=False, ddp_static_graph=False, use_bn_sync=False, device="cpu",
+                  skip_scheduler=False, balanced_mixup=0.5, num_classes=2, grad_clip_norm=1.0,
+                  log_every_n_steps=1, world_size=1, batch_size=4)
+TRAIN_BATCHES, TRAIN_B, MIX_SEED = 3, 4, 321
+
+
+def gen_train(ref_scan):
+    import json
+    import tempfile
+    from functools import partial
+    from types import SimpleNamespace
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(HERE))
+    import toy_models as T
+    import_reference_model(ref_scan)           # stubs for open_clip & co, then pipeline imports
+    import importlib
+    pipeline = importlib.import_module("mamba_clip.pipeline")
+    ref_train = importlib.import_module("mamba_clip.train")
+    ref_loss = importlib.import_module("mamba_clip.loss")
+    for kind in ("clip", "classifier"):
+        torch.manual_seed(7)
+        model = T.ToyClip() if kind == "clip" else T.ToyClassifier()
+        init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        data = {"train": T.ToyData(T.toy_batches(TRAIN_BATCHES, TRAIN_B, seed=11), TRAIN_B)}
+        with tempfile.TemporaryDirectory() as logs:
+            os.makedirs(os.path.join(logs, "toy"))
+            args = SimpleNamespace(**TRAIN_ARGS, logs=logs)
+            params, args = pipeline.prepare_params(model, data, torch.device("cpu"), args)
+        opt, sched = params["optimizer"], params["scheduler"]
+        ids = {id(p): n for n, p in model.named_parameters()}
+        groups = [[ids[id(p)] for p in g["params"]] for g in opt.param_groups]
+        lrs, losses = [], []
+
+        def rec_sched(step, _s=sched):
+            lrs.append(float(_s(step)))
+
+        inner = (ref_loss.ClipLoss() if kind == "clip"
+                 else partial(ref_loss.cross_entropy_loss, weight=torch.tensor([1.0, 3.0])))
+
+        def rec_loss(**kw):
+            out = inner(**kw)
+            losses.append(float((out["contrastive_loss"] if isinstance(out, dict) else out).detach()))
+            return out
+
+        np.random.seed(MIX_SEED)
+        for epoch in range(args.epochs):
+            ref_train.train_one_epoch(model, data, rec_loss, epoch, opt, params["scaler"], rec_sched, args)
+        tensors = {f"init.{k}": v.contiguous() for k, v in init_sd.items()}
+        tensors.update({f"final.{k}": v.detach().contiguous() for k, v in model.state_dict().items()})
+        tensors["losses"] = torch.tensor(losses, dtype=torch.float64)
+        tensors["lrs"] = torch.tensor(lrs, dtype=torch.float64)
+        meta = {"groups": json.dumps(groups), "kind": kind, "mix_seed": str(MIX_SEED),
+                "args": json.dumps({k: v for k, v in TRAIN_ARGS.items() if k != "logs"})}
+        save_file(tensors, os.path.join(HERE, f"train_{kind}_mixup.safetensors"), metadata=meta)
+        print("wrote train", kind, losses)
+
+    # schedulers: (factory, positional args after the optimizer) -> lr at steps 0..39
+    sched_mod = importlib.import_module("mamba_clip.scheduler")
+
+    class _Opt:
+        def __init__(self):
+            self.param_groups = [{"lr": 0.0}]
+    cases = {
+        "cosine": ("cosine_lr", (1e-3, 5, 40), {}),
+        "cosine_restart": ("cosine_lr", (1e-3, 3, 40), {"restart_interval": 13}),
+        "const": ("const_lr", (2e-3, 7, 40), {}),
+        "const_restart": ("const_lr", (2e-3, 4, 40), {"restart_interval": 9}),
+        "cooldown": ("const_lr_cooldown", (1e-3, 5, 40, 10), {"cooldown_power": 2.0, "cooldown_end_lr": 1e-5}),
+        "cooldown_restart": ("const_lr_cooldown", (1e-3, 2, 40, 4), {"restart_interval": 10}),
+    }
+    tensors = {}
+    for name, (fn, pos, kw) in cases.items():
+        o = _Opt()
+        f = getattr(sched_mod, fn)(o, *pos, **kw)
+        vals = []
+        for s in range(40):
+            r = f(s)
+            assert r == o.param_groups[0]["lr"]
+            vals.append(float(r))
+        tensors[name] = torch.tensor(vals, dtype=torch.float64)
+    import json as _j
+    save_file(tensors, os.path.join(HERE, "schedulers.safetensors"),
+              metadata={"cases": _j.dumps({k: [v[0], list(v[1]), v[2]] for k, v in cases.items()})})
+    print("wrote schedulers")
+
+
+GENERATORS = {"scan": lambda r: gen_scan(r), "loss": lambda r: gen_loss(), "ss2d": gen_ss2d, "c1": gen_c1,
+              "train": gen_train}
+
 if __name__ == "__main__":
     ref_scan = load_reference_scan()
-    gen_scan(ref_scan)
-    gen_loss()
-    gen_ss2d(ref_scan)
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name](ref_scan)

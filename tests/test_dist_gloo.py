@@ -4,8 +4,12 @@ label offsets and loss coefficients, gather_with_grad -- against the golden
 vectors produced by the reference loss.py under gloo (tests/golden).
 
 The HIP kernels cannot run on CPU, so here the dense op `scaled_logits_ce`
-is replaced by a CPU restatement (the oracle acts as the checker); the same
-op is checked against the oracle on the GPU in test_loss_gpu.py."""
+is replaced by a CPU restatement (the oracle acts as the checker).  The HIP
+op itself is checked on the GPU in test_loss_gpu.py on every path this host
+logic drives: square global logits, and the local_loss rectangular (b x N)
+logits with row offset b*rank and no column term
+(test_scaled_logits_ce_local_loss_rectangular, and per rank against these same
+gloo goldens in test_local_loss_matches_reference_gloo_golden)."""
 import os
 import socket
 
@@ -160,3 +164,77 @@ def test_ddp_train_step_matches_single_process_gloo_w2():
     scale = np.abs(ref).max()
     np.testing.assert_allclose(g[1:], ref[1:], rtol=1e-4, atol=1e-6 * scale)
     np.testing.assert_allclose(g[0] / world, ref[0], rtol=1e-4)
+
+
+# ---------------------------------------------------------------- stage-2 head under DDP (pipeline.py:587-636)
+def _stage2_worker(rank, world, port, q):
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+        from functools import partial
+        from types import SimpleNamespace
+        import torch.distributed as dist
+        from mamba_clip_amd.loss import cross_entropy_loss
+        from mamba_clip_amd.model import ClipClassifier, build_clip
+        from mamba_clip_amd.train import create_optimizer, train_step, wrap_ddp
+        from oracle.cpu_model import oracle_ops
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        args = SimpleNamespace(precision="fp32", lr=1e-3, wd=0.1, beta1=0.9, beta2=0.98, eps=1e-8,
+                               grad_clip_norm=None, distributed=True, ddp_static_graph=False, rank=rank,
+                               world_size=world)
+        g = torch.Generator().manual_seed(9)
+        B = 4 * world
+        images = torch.randn(B, 3, 32, 32, generator=g)
+        texts = torch.randint(1, 999, (B, 16), generator=g)
+        targets = torch.randint(0, 2, (B,), generator=g)
+        sl = slice(rank * 4, (rank + 1) * 4)
+        loss = partial(cross_entropy_loss, weight=torch.tensor([1.0, 2.0]))
+        with oracle_ops():
+            torch.manual_seed(0)
+            head = ClipClassifier(build_clip("tiny-mamba-clip"), num_classes=2)
+            init = {k: v.clone() for k, v in head.state_dict().items()}
+            model = wrap_ddp(head, args, torch.device("cpu"))
+            opt = create_optimizer(model, args)
+            n_train = sum(p.numel() for p in model.parameters() if p.requires_grad)
+            logits = model(images[sl], texts[sl])
+            loss(logits, targets[sl]).backward()
+            grads = torch.cat([p.grad.flatten() for p in model.module.fc.parameters()])
+            opt.zero_grad()
+            train_step(model, images[sl], texts[sl], targets[sl], loss, opt, None, args)
+            res = {"params": torch.cat([p.detach().flatten() for p in model.module.parameters()]).numpy(),
+                   "grads": grads.numpy(), "n_train": n_train}
+            if rank == 0:   # one process over the whole global batch, same init
+                ref = ClipClassifier(build_clip("tiny-mamba-clip"), num_classes=2)
+                ref.load_state_dict(init)
+                loss(ref(images, texts), targets).backward()
+                res["ref_grads"] = torch.cat([p.grad.flatten() for p in ref.fc.parameters()]).numpy()
+                res["fc_numel"] = sum(p.numel() for p in ref.fc.parameters())
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+def test_stage2_head_ddp_gloo_w2():
+    """Stage 2 as replicas: only the head trains, DDP all-reduces just the head's gradients
+    (identical on both ranks after the all-reduce) and the replicas stay bit-identical after the step."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stage2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+    np.testing.assert_array_equal(out[0]["params"], out[1]["params"])
+    np.testing.assert_array_equal(out[0]["grads"], out[1]["grads"])
+    assert out[0]["n_train"] == out[0]["fc_numel"]           # frozen towers: only the fc head is trained
+    assert np.isfinite(out[0]["grads"]).all() and np.abs(out[0]["grads"]).max() > 0

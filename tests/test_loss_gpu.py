@@ -81,3 +81,69 @@ def test_get_logits_matches_reference_semantics():
     li, lt = ClipLoss().get_logits(img.to(DEV), txt.to(DEV), torch.tensor(2.0, device=DEV))
     torch.testing.assert_close(li.cpu(), 2 * img @ txt.T, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(lt.cpu(), 2 * txt @ img.T, rtol=1e-5, atol=1e-4)
+
+
+def _ce_oracle(X, Y, scale, row_off, coef_r, col_off=0, coef_c=0.0):
+    """fp64 restatement of the dense part of ClipLoss (loss.py:102-145): rows i -> label i + row_off,
+    columns j -> label j + col_off."""
+    S = scale * X @ Y.T
+    r = torch.arange(S.shape[0])
+    loss = coef_r * (torch.logsumexp(S, 1) - S[r, r + row_off]).sum()
+    if coef_c:
+        c = torch.arange(S.shape[1])
+        loss = loss + coef_c * (torch.logsumexp(S, 0) - S[c + col_off, c]).sum()
+    return loss
+
+
+@pytest.mark.parametrize("b,world,E", [(5, 3, 64), (64, 8, 512), (7, 2, 24), (130, 4, 512)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_scaled_logits_ce_local_loss_rectangular(b, world, E, dtype):
+    """The local_loss path (loss.py:80-81, 101-103) on the HIP kernels: rectangular (b x N) logits,
+    row labels offset by b*rank, no column term; loss, dX, dY and d(scale) vs fp64, every rank."""
+    from mamba_clip_amd.ops import scaled_logits_ce
+    N = b * world
+    g = torch.Generator().manual_seed(b * 1000 + world)
+    Yall = torch.nn.functional.normalize(torch.randn(N, E, generator=g), dim=-1).to(dtype)
+    Xall = torch.nn.functional.normalize(torch.randn(N, E, generator=g), dim=-1).to(dtype)
+    for rank in range(world):
+        X = Xall[rank * b:(rank + 1) * b]
+        xr = X.double().requires_grad_(True)
+        yr = Yall.double().requires_grad_(True)
+        sr = torch.tensor(12.5, dtype=torch.float64, requires_grad=True)
+        ref = _ce_oracle(xr, yr, sr, b * rank, 0.5 / b)
+        ref.backward()
+        xd = X.to(DEV).requires_grad_(True)
+        yd = Yall.to(DEV).requires_grad_(True)
+        sd = torch.tensor(12.5, device=DEV, requires_grad=True)
+        loss = scaled_logits_ce(xd, yd, sd, b * rank, 0.5 / b)
+        loss.backward()
+        tol = 1e-5 if dtype == torch.float32 else 1e-3
+        assert abs(float(loss) - float(ref)) <= tol * abs(float(ref)) + 1e-6, (rank, float(loss), float(ref))
+        for got, want in ((xd.grad, xr.grad), (yd.grad, yr.grad)):
+            scale = float(want.abs().max())
+            err = float((got.double().cpu() - want).abs().max())
+            assert err <= (1e-5 if dtype == torch.float32 else 1e-2) * scale, (rank, err, scale)
+        assert abs(float(sd.grad) - float(sr.grad)) <= tol * abs(float(sr.grad)) + 1e-5
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_local_loss_matches_reference_gloo_golden(world):
+    """Per rank, ClipLoss(local_loss=True)'s dense math on the HIP kernels (the feature gather done
+    from the golden's global features) equals the reference's gloo results ll1_gg0 (loss.py as-is)."""
+    from mamba_clip_amd.ops import scaled_logits_ce
+    g = load_golden(f"clip_loss_gloo_w{world}.safetensors")
+    b = g["img"].shape[0] // world
+    all_i, all_t = g["img"].to(DEV), g["txt"].to(DEV)
+    for rank in range(world):
+        img = all_i[rank * b:(rank + 1) * b].clone().requires_grad_(True)
+        txt = all_t[rank * b:(rank + 1) * b].clone().requires_grad_(True)
+        s = torch.tensor(10.0, device=DEV, requires_grad=True)
+        # loss.py:105-108 local branch; gathered copies carry no grad (gather_with_grad False)
+        loss = (scaled_logits_ce(img, all_t, s, b * rank, 0.5 / b)
+                + scaled_logits_ce(txt, all_i, s, b * rank, 0.5 / b))
+        loss.backward()
+        key = f"r{rank}.ll1_gg0"
+        torch.testing.assert_close(loss.detach().cpu().reshape(1), g[f"{key}.loss"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(img.grad.cpu(), g[f"{key}.grad_img"], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(txt.grad.cpu(), g[f"{key}.grad_txt"], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(s.grad.cpu().reshape(1), g[f"{key}.grad_scale"], rtol=1e-4, atol=1e-6)

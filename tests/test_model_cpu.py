@@ -101,3 +101,108 @@ def test_split_k_projection_autograd_cpu():
     assert torch.autograd.gradcheck(lambda w, X: wleft_mm(w, X), (w, X))
     H = torch.randn(64, 16, dtype=torch.float64, requires_grad=True)
     assert torch.autograd.gradcheck(lambda w, H: wleft_mm(w, H.t()), (w, H))
+
+
+# ---------------------------------------------------------------- boundary fidelity (model.py:998-1112, 1257-1289)
+def test_clip_model_reference_constructor_shares_logit_params():
+    """ClipModel(model) shares the towers and logit_scale / logit_bias (model.py:1001-1009), and
+    init_model(..., is_clip=True) keeps a learned temperature (model.py:1274-1275)."""
+    import math
+    import torch.nn as nn
+    from mamba_clip_amd.model import ClipModel
+
+    base = build_clip("tiny-mamba-clip")
+    with torch.no_grad():
+        base.logit_scale.fill_(3.3)
+    base.logit_bias = nn.Parameter(torch.tensor(-2.0))
+    wrapped = ClipModel(base)
+    assert wrapped.visual is base.visual and wrapped.text is base.text
+    assert wrapped.logit_scale is base.logit_scale and wrapped.logit_bias is base.logit_bias
+    assert wrapped.context_length == 16 and wrapped.vocab_size == 1000
+
+    class Raw(nn.Module):                   # an open_clip-like CLIP that is not a ClipModel
+        def __init__(self):
+            super().__init__()
+            self.visual, self.text = base.visual, base.text
+            self.logit_scale = nn.Parameter(torch.tensor(2.5))
+            self.logit_bias = None
+    m, _, _, _ = init_model(Raw, is_clip=True)
+    assert isinstance(m, ClipModel) and float(m.logit_scale) == 2.5 and m.logit_bias is None
+    fresh = ClipModel(base.visual, base.text)
+    assert abs(float(fresh.logit_scale) - math.log(1 / 0.07)) < 1e-6 and fresh.logit_bias is None
+
+
+def test_lock_text_tower_freezes_embeddings_and_layers():
+    """model.py:1072-1097: full lock freezes embeddings + every layer (norms follow freeze_layer_norm);
+    unlocked_layers=k freezes [embeddings, *layers][:-k]; the projection stays trainable."""
+    def trainable(m):
+        return {n for n, p in m.text.named_parameters() if p.requires_grad}
+
+    m = build_clip("tiny-mamba-clip")                          # Mamba text: 2 layers
+    m.lock_text_tower()
+    assert trainable(m) == {"proj.weight"}
+    m = build_clip("tiny-mamba-clip")
+    m.lock_text_tower(freeze_layer_norm=False)
+    assert trainable(m) == {"proj.weight", "norm_f", "layers.0.norm_weight", "layers.1.norm_weight"}
+    m = build_clip("tiny-mamba-clip")
+    m.lock_text_tower(unlocked_layers=1)
+    t = trainable(m)
+    assert "embedding.weight" not in t and not any(n.startswith("layers.0.") for n in t)
+    assert any(n.startswith("layers.1.") for n in t) and "norm_f" in t and "proj.weight" in t
+    from mamba_clip_amd.model import BertTextEncoder, ClipModel, VisionTransformer
+    bm = ClipModel(VisionTransformer(img_size=32, patch=8, width=64, layers=1, heads=4, output_dim=16),
+                   BertTextEncoder(vocab_size=100, context_length=8, width=64, layers=2, heads=4, output_dim=16))
+    bm.lock_text_tower(unlocked_layers=1)
+    t = trainable(bm)
+    assert not {"tok.weight", "pos", "ln.weight"} & t and not any(n.startswith("blocks.0.") for n in t)
+    assert any(n.startswith("blocks.1.") for n in t) and any(n.startswith("proj.") for n in t)
+
+
+def test_ss2d_parameter_inits_follow_reference_statistics():
+    """model.py:437-501: dt_proj weight ~ U(+-dt_rank^-0.5), softplus(dt bias) ~ logU[1e-3, 1e-1]
+    (floored 1e-4), A_logs = log(1..N) per channel (S4D-real), Ds = 1, x_proj kaiming-uniform."""
+    import math
+    import torch.nn.functional as F
+    from mamba_clip_amd.model import SS2D
+    torch.manual_seed(0)
+    m = SS2D(d_model=128)
+    R, di, N = m.dt_rank, m.d_inner, m.d_state
+    assert (R, di, N) == (8, 256, 16)
+    w = m.dt_projs_weight
+    assert w.shape == (4, di, R) and float(w.abs().max()) <= R ** -0.5 + 1e-7
+    assert abs(float(w.std()) - R ** -0.5 / math.sqrt(3)) < 0.02 * R ** -0.5
+    dt = F.softplus(m.dt_projs_bias)
+    assert dt.shape == (4, di) and float(dt.min()) >= 1e-4 * 0.999 and float(dt.max()) <= 0.1 * 1.001
+    # log-uniform: log dt is uniform on [log 1e-3, log 1e-1] -> mean at the midpoint, std (range)/sqrt(12)
+    lg = dt.log()
+    mid, rng = (math.log(1e-3) + math.log(1e-1)) / 2, math.log(1e-1) - math.log(1e-3)
+    assert abs(float(lg.mean()) - mid) < 0.05 * rng and abs(float(lg.std()) - rng / math.sqrt(12)) < 0.05 * rng
+    torch.testing.assert_close(m.A_logs, torch.log(torch.arange(1, N + 1).float()).repeat(4 * di, 1))
+    assert torch.equal(m.Ds, torch.ones(4 * di))
+    bound = 1 / math.sqrt(di)                       # kaiming_uniform(a=sqrt(5)) on fan_in = d_inner
+    assert m.x_proj_weight.shape == (4, R + 2 * N, di) and float(m.x_proj_weight.abs().max()) <= bound + 1e-7
+
+
+def test_ss2d_c1_shape_cpu_restatement_matches_reference_golden():
+    """Our SS2D module wiring at C1's exact shape (d_model 128, 8x16x16) with the CPU restatement ops,
+    against the reference SS2D golden -- the GPU test runs the same fixture on the HIP path."""
+    from conftest import load_golden
+    from mamba_clip_amd.model import SS2D
+    from oracle.cpu_model import oracle_ops
+    g = load_golden("ss2d_c1_d128_h16w16.safetensors")
+    gen = torch.Generator().manual_seed(2025)
+    x = torch.randn(8, 16, 16, 128, generator=gen)
+    gy = torch.randn(8, 16, 16, 128, generator=gen)
+    chk = torch.stack([x.double().sum(), x.double().abs().sum(), gy.double().sum()])
+    torch.testing.assert_close(chk, g["x_checksum"], rtol=0, atol=0)
+    m = SS2D(d_model=128).eval()
+    m.load_state_dict({k[3:]: v for k, v in g.items() if k.startswith("sd.")})
+    xg = x.requires_grad_(True)
+    with oracle_ops():
+        y = m(xg)
+        y.backward(gy)
+    torch.testing.assert_close(y.detach(), g["y"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(xg.grad, g["gx"], rtol=1e-3, atol=1e-5)
+    for n, p in m.named_parameters():
+        ref = g[f"grad.{n}"]
+        torch.testing.assert_close(p.grad, ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max()), msg=n)
