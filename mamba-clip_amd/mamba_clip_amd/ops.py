@@ -343,15 +343,32 @@ def causal_conv1d(x, weight, bias=None, silu=True):
     return CausalConv1dFn.apply(x, weight, bias, silu)
 
 
+class PatchIm2colFn(torch.autograd.Function):
+    """Non-overlapping (k = s = P) patch rows.  The map is a permutation of the image, so the
+    backward is the inverse permutation (one strided copy): VSSM's input gradient
+    (model.py:189-201) flows through it."""
+
+    @staticmethod
+    def forward(ctx, img, patch):
+        lib = _lib.load()
+        img = img.contiguous()
+        Bsz, C, H, W = img.shape
+        out = torch.empty(Bsz * (H // patch) * (W // patch), C * patch * patch, device=img.device, dtype=img.dtype)
+        _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(img.dtype), img.data_ptr(),
+                                       out.data_ptr(), _lib.stream_handle(img.device)), "mc_patch_im2col")
+        ctx.meta = (Bsz, C, H, W, patch)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        Bsz, C, H, W, P = ctx.meta
+        gi = g.reshape(Bsz, H // P, W // P, C, P, P).permute(0, 3, 1, 4, 2, 5).reshape(Bsz, C, H, W)
+        return gi, None
+
+
 def patch_im2col(img, patch):
-    """(B, C, H, W) -> (B * H/P * W/P, C * P * P) patch rows (no autograd: image inputs)."""
-    lib = _lib.load()
-    img = img.contiguous()
-    Bsz, C, H, W = img.shape
-    out = torch.empty(Bsz * (H // patch) * (W // patch), C * patch * patch, device=img.device, dtype=img.dtype)
-    _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(img.dtype), img.data_ptr(), out.data_ptr(),
-                                   _lib.stream_handle(img.device)), "mc_patch_im2col")
-    return out
+    """(B, C, H, W) -> (B * H/P * W/P, C * P * P) patch rows (row = (b, h/P, w/P), col = (c, ph, pw))."""
+    return PatchIm2colFn.apply(img, patch)
 
 
 # ---------------------------------------------------------------------------- projections with split-K weight grads

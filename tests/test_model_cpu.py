@@ -206,3 +206,27 @@ def test_ss2d_c1_shape_cpu_restatement_matches_reference_golden():
     for n, p in m.named_parameters():
         ref = g[f"grad.{n}"]
         torch.testing.assert_close(p.grad, ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max()), msg=n)
+
+
+def test_vssm_tiny_cpu_restatement_matches_reference_golden():
+    """Our VSSM wiring (PatchEmbed2D im2col incl. its inverse-permutation backward, PatchMerging2D,
+    SS_Conv_SSM stages, avgpool head) with the CPU restatement ops vs the reference VSSM golden."""
+    from conftest import load_golden
+    from mamba_clip_amd.model import VSSM
+    from mamba_clip_amd.ops import PatchIm2colFn
+    from oracle.cpu_model import oracle_ops
+    g = load_golden("vssm_tiny_d16.safetensors")
+    m = VSSM(patch_size=4, in_chans=3, num_classes=2, depths=[1, 1, 2, 1], dims=[16, 32, 64, 128]).eval()
+    m.load_state_dict({k[3:]: v for k, v in g.items() if k.startswith("sd.")})
+    x = g["x"].clone().requires_grad_(True)
+    with oracle_ops():
+        y = m(x)
+        y.backward(g["gy"])
+    torch.testing.assert_close(y.detach(), g["y"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(x.grad, g["gx"], rtol=1e-3, atol=1e-6)
+    torch.testing.assert_close(m.head.weight.grad, g["grad.head.weight"], rtol=1e-3, atol=1e-6)
+    # the product im2col's backward is the exact inverse permutation of the unfold layout
+    img = torch.randn(2, 3, 8, 12, dtype=torch.float64)
+    cols = torch.nn.functional.unfold(img, 4, stride=4).transpose(1, 2).reshape(-1, 48)
+    back = PatchIm2colFn.backward(type("C", (), {"meta": (2, 3, 8, 12, 4)})(), cols)[0]
+    assert torch.equal(back, img)
