@@ -51,10 +51,16 @@ enum {
   MC_ERR_WORKSPACE = -5  /* workspace too small */
 };
 
+/* States are held in VGPRs, one channel per lane: dstate <= 32 (padded to 8/16/32).
+ * Upstream mamba_ssm accepts up to 256; every reference call site and BASELINE
+ * config uses 16 (model.py:357, 539-550).  Larger dstate returns MC_ERR_SHAPE. */
 #define MC_SCAN_MAX_DSTATE 32
-/* sequence positions per saved chunk state (training forward writes the state
- * after every MC_SCAN_CHUNK positions; the backward resumes from them) */
-#define MC_SCAN_CHUNK 8
+/* sequence positions per saved chunk state: the training forward writes the
+ * fp32 state after every MC_SCAN_CHUNK positions (and after the last position);
+ * the backward walks chunks of this length in reverse, recomputing the states
+ * inside a chunk from the one saved at its start.  32 positions = 2 B per
+ * (channel, position) at dstate 16, a quarter of the bf16 activations. */
+#define MC_SCAN_CHUNK 32
 
 typedef struct mc_scan_fwd_params {
   int32_t batch, dim, seqlen, dstate, n_groups;
@@ -77,13 +83,14 @@ typedef struct mc_scan_fwd_params {
   const void* z;            /* nullable: out = (y + D u) * silu(z) */
   const float* delta_bias;  /* nullable, (dim,) */
   void* out;
-  float* chunk_states;      /* nullable: (batch, dim, n_chunks, dstate) fp32, state at END of each chunk */
+  float* chunk_states;      /* nullable: (batch, dim, n_chunks, dstate) fp32, state at END of each chunk
+                               (the last entry: the state after position seqlen-1) */
   float* last_state;        /* nullable: (batch, dim, dstate) fp32 */
   void* workspace;          /* >= mc_scan_fwd_workspace_bytes(...) bytes, 16-B aligned */
   size_t workspace_bytes;
   /* nullable; used only when z is given: the pre-gate output y + D u (itype,
-   * seqlen stride 1) -- the `out` upstream's forward returns next to out_z and
-   * its backward takes for dz.  A training caller passes it on to mc_scan_bwd. */
+   * seqlen stride 1) -- the `out` upstream's forward returns next to out_z.
+   * Not needed for training: mc_scan_bwd recomputes y for dz. */
   void* out_y;
   int64_t out_y_batch_stride, out_y_dim_stride;
 } mc_scan_fwd_params;
@@ -127,8 +134,8 @@ typedef struct mc_scan_bwd_params {
   float* ddelta_bias;
   void* workspace;            /* >= mc_scan_bwd_workspace_bytes(...) bytes, 256-B aligned */
   size_t workspace_bytes;
-  /* REQUIRED when z is given: the forward's pre-gate output (mc_scan_fwd_params.out_y),
-   * as upstream's bwd takes `out` for dz = dout * out * silu'(z) */
+  /* ignored (kept for layout stability): the backward recomputes the pre-gate
+   * output y + D u that dz = dout * y * silu'(z) needs from the chunk states */
   const void* out_y;
   int64_t out_y_batch_stride, out_y_dim_stride;
 } mc_scan_bwd_params;

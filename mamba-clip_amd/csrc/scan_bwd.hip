@@ -9,28 +9,29 @@
 //   du_t  = D gy_t + sum_n h_t,n dt_t B_t,n
 //   ddt_t = sum_n h_t,n (A_n a_t,n x_{t-1,n} + B_t,n u_t),  ddelta_t = ddt_t * sigmoid(delta_t + bias)
 //   dA_n  = sum_{b,t} h_t,n dt_t a_t,n x_{t-1,n}    dD = sum gy u    dbias = sum ddelta
+//   (y_t = sum_n C_t,n x_t,n + D u_t is recomputed here; the forward stores no pre-gate output)
 //
-// Design (DESIGN.md "scan_bwd"):
-//  * one wave = 64 channels of one (batch, group); tiles of kTB = kS = 8
-//    positions walked in reverse; each tile restarts from the fp32 state the
-//    training forward saved at its start (chunk_states), so nothing is
-//    recomputed across tiles and no mid-tile pre-pass is needed.
-//  * state pairs (n, n+1) in packed fp32; the pair loop is fully unrolled, so
-//    A, the adjoint carry and the dA accumulators of every pair stay in VGPRs.
-//    Per pair and tile: a forward sweep (x, a kept in VGPRs), the reverse
-//    adjoint sweep; per-position accumulators carried across pairs:
-//      S_t = sum_n h B,  Q_t = sum_n h A a x_{t-1},  y_t = sum_n C x
-//    so du = dt S + D gy and ddt = (Q + u S) sigmoid need no per-n work.
-//  * each lane reads / writes its own row's positions as 16-B vectors; the
-//    next tile's rows, B/C quads and saved state are prefetched into
-//    registers under the current tile.  The tile's B/C block sits in LDS as
-//    [pair][position]{B_n, B_n+1, C_n, C_n+1}: one broadcast ds_read_b128.
-//  * dB/dC (sums over the 64 channels of the wave) use an in-register
-//    transpose-reduce: permlane32_swap / permlane16_swap / DPP row_ror:8 /
-//    ds_swizzle / quad_perm halving stages turn 16 per-lane values into 16
-//    wave sums in ~2.5 VALU per value, then land in a per-wave fp32 slab.  A
-//    small second kernel sums the slabs over waves / batches: deterministic,
-//    no atomics.
+// Design:
+//  * A workgroup = TWO waves on the same 64 channels of one (batch, group).
+//    The state pairs (n, n+1) are split between the waves (kN/4 pairs each),
+//    so the rows and the B/C block staged in LDS serve both, and each wave's
+//    per-pair state fits in registers.  2 waves/SIMD at 16-bit I/O.
+//  * The sequence is walked in reverse in chunks of kTC = 32 positions -- the
+//    forward's saved-state interval (MC_SCAN_CHUNK).  Each chunk's rows of
+//    u / delta / z / dout are fetched with coalesced 16-B loads (whole 64-B
+//    row segments per 4 lanes), prefetched into registers one chunk ahead,
+//    and transposed through LDS (XOR-swizzled: conflict-free own-row reads).
+//  * Inside a chunk, the states at the starts of its four 8-position
+//    sub-tiles are recomputed from the saved chunk state (a forward sweep over
+//    24 positions, kept in LDS), then the sub-tiles are processed in reverse:
+//    per pair a forward sweep (x, a kept in VGPRs), the dC reduction, the
+//    reverse adjoint sweep and the dB reduction (in-register transpose-reduce).
+//  * Per-position sums over the pairs (S = sum h B, Q = sum h A a x, Y = sum C x)
+//    are exchanged between the two waves through LDS; each wave finishes four
+//    of the sub-tile's positions, writes du / ddelta / dz over the consumed LDS
+//    rows, and the chunk's outputs leave as coalesced 16-B stores.
+//  * dB / dC per sub-tile go to a per-workgroup slab (one coalesced 16-B store
+//    per lane); small second kernels sum the slabs: deterministic, no atomics.
 #include <cstdlib>
 #include <type_traits>
 
@@ -39,21 +40,24 @@
 namespace mc {
 namespace scan {
 
-constexpr int kTB = kS;  // positions per backward tile (== saved-state granularity)
+constexpr int kTC = kS;          // positions per backward chunk == saved-state interval (32)
+constexpr int kTB = 8;           // positions per sub-tile (the pair loop's register tile)
+constexpr int kSub = kTC / kTB;  // sub-tiles per chunk
+constexpr int kWG = 2 * kRows;   // threads per workgroup: two waves
+static_assert(kTC % kTB == 0, "chunk must be whole sub-tiles");
 
 struct BwdArgs {
   int batch, dim, seqlen, dstate, n_groups, n_states, nblk, total_blocks, softplus;
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, go_bs, go_ds;
   int64_t du_bs, du_ds, ddt_bs, ddt_ds, dz_bs, dz_ds;  // output strides (seqlen stride 1)
   const void* u; const void* delta; const void* z; const void* dout;
-  const float* A; const float* bct; const float* D; const float* delta_bias;
+  const float* A; const float* bq; const float* D; const float* delta_bias;
   const float* chunk_states;
   void* du; void* ddelta; void* dz;
   float* slab_bc;                    // [b*G+g][nblk][seqlen][2][kN]  (dB partials, then dC partials)
   float* slab_a;                     // [b][kN][dim] (dA partials, one owner per element)
   float* slab_d;                     // [b][dim]
   float* slab_bias;                  // [b][dim]
-  const void* y; int64_t y_bs, y_ds;  // forward's pre-gate output (required with z)
 };
 
 __device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
@@ -100,7 +104,7 @@ __device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane)
   }
   if constexpr (NV >= 16) {
 #pragma unroll
-    for (int j = 0; j < NV / 16; ++j) {   // lane bit 2 via ds_swizzle xor 4
+    for (int j = 0; j < NV / 16; ++j) {   // lane bit 2 via xor 4
       const float keep = b2 ? v[j + NV / 16] : v[j], send = b2 ? v[j] : v[j + NV / 16];
       v[j] = keep + dpp_f(send, 1);
     }
@@ -116,70 +120,54 @@ __device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane)
   return v[0] + dpp_f(v[0], 3);         // lane bit 0 via quad_perm [1,0,3,2]
 }
 
-// Own-row vector I/O: a lane reads / writes the kTB consecutive positions of
-// its own (b, d) row as 16-B vectors (no LDS staging of the rows: a wave
-// revisits its rows tile after tile, so L2 sees whole lines).  Addresses are a
-// wave-uniform base (SGPRs) + a 32-bit per-lane element offset, so each row
-// costs one VGPR instead of a 64-bit pointer pair (the host checks the range).
-template <typename TI>
-__device__ __forceinline__ void load_row_tile(const TI* __restrict__ base, uint32_t off, int l0, int L, bool full,
-                                              uint4 (&q)[kTB / ElemTraits<TI>::kVec]) {
-  constexpr int VI = ElemTraits<TI>::kVec;
-#pragma unroll
-  for (int k = 0; k < kTB / VI; ++k) {
-    const int col0 = l0 + k * VI;
-    const TI* p = base + (uint32_t)(off + col0);
-    if (full) q[k] = ld16(p);
-    else q[k] = ld16_masked(p, max(0, min(VI, L - col0)));
-  }
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations are
+// complete, global loads / stores stay in flight (gfx950 has the back-off
+// barrier, so s_barrier itself forces no vmcnt drain; __syncthreads()'s fence
+// would wait for every prefetch still in flight).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
+// LDS image of one array's chunk rows: 64 rows x RB bytes, 16-B blocks XOR-
+// swizzled by row so that 64 lanes reading their own rows at one column hit
+// distinct bank groups (ds_read_b128 lane groups) and the staging writes
+// (8 lanes = 2 whole rows) are contiguous.
 template <typename TI>
-__device__ __forceinline__ void store_row_tile(TI* __restrict__ base, uint32_t off, int l0, int L, bool full,
-                                               const float (&v)[kTB]) {
-  constexpr int VI = ElemTraits<TI>::kVec;
-#pragma unroll
-  for (int k = 0; k < kTB / VI; ++k) {
-    float w[VI];
-#pragma unroll
-    for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
-    const int col0 = l0 + k * VI;
-    TI* p = base + (uint32_t)(off + col0);
-    if (full) st16(p, pack_f<TI>(w));
-    else st16_masked(p, pack_f<TI>(w), max(0, min(VI, L - col0)));
-  }
-}
+struct ChunkRows {
+  static constexpr int RB = kTC * (int)sizeof(TI);   // bytes per row segment: 64 (16-bit) / 128 (fp32)
+  static constexpr int VPR = RB / 16;                // 16-B vectors per row segment
+  static constexpr int kShift = VPR == 4 ? 2 : 1;
+  static constexpr int kBytes = kRows * RB;
+  __device__ static __forceinline__ int off(int r, int c) { return r * RB + ((c ^ ((r >> kShift) & (VPR - 1))) << 4); }
+};
 
-// One wave = 64 channels of one (batch, group); tiles of kTB = 8 positions in
-// reverse; state PAIRS (n, n+1) are the unit of work, in packed fp32
-// (v_pk_mul_f32 / v_pk_fma_f32), fully unrolled over the kN / 2 pairs so the
-// per-pair lane constants (A, the adjoint carry, the dA accumulator) live in
-// VGPRs.  Per pair and tile: a forward sweep from the saved tile-start state
-// (decays and states kept in VGPRs), the dC contributions reduced across the
-// wave, then the reverse adjoint sweep and the dB reduction.  The tile's B/C
-// block is staged in LDS as [pair][position]{B_n, B_n+1, C_n, C_n+1} so one
-// broadcast ds_read_b128 serves a (pair, position).  The next tile's rows,
-// B/C block and saved state are prefetched into registers under this tile.
-template <typename TI, int kN, bool kAligned, int kGrp>
-__global__ __launch_bounds__(kRows, kGrp >= 4 ? 1 : 2) void scan_bwd_kernel(const BwdArgs a) {
-  constexpr int VI = ElemTraits<TI>::kVec;
-  constexpr int kVT = kTB / VI;            // 16-B vectors per row tile (1 for 16-bit, 2 for fp32)
-  constexpr int kP = kN / 2;               // state pairs
-  constexpr int kBCQ = kP * kTB;           // (pair, position) quads of one tile
-  constexpr int kBCPer = (kBCQ + kRows - 1) / kRows;
+template <typename TI, int kN, bool kAligned, bool kSP, int kMinW>
+__global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
+  using CR = ChunkRows<TI>;
+  constexpr int VI = ElemTraits<TI>::kVec;   // elements per 16-B vector
+  constexpr int VPR = CR::VPR;
+  constexpr int kVT = kTB / VI;              // 16-B vectors per sub-tile row (1 for 16-bit, 2 for fp32)
+  constexpr int kP = kN / 2;                 // state pairs
+  constexpr int kPW = kP / 2;                // pairs per wave
+  constexpr int kQC = kTC * kP;              // B/C quads per chunk
+  constexpr int kQPer = (kQC + kWG - 1) / kWG;
+  constexpr int kEH = kTB / 2;               // positions of a sub-tile each wave finishes
+  static_assert(kPW >= 2 && kPW % 2 == 0, "kN in {8, 16, 32}");
 
-  extern __shared__ __attribute__((aligned(16))) float smem_f[];
-  f32x4* bcq = reinterpret_cast<f32x4*>(smem_f);   // [kP][kTB] B/C quads of the tile
-  // per-lane, per-pair scalars that persist across pairs / tiles live in LDS
-  // ([pair][lane] f32x2: conflict-free ds_read_b64), read and written once per
-  // pair and tile -- keeps the fully unrolled pair loop within 256 VGPRs
-  f32x2* carry_s = reinterpret_cast<f32x2*>(bcq + kBCQ);   // adjoint carried into the previous tile
-  f32x2* dA_s = carry_s + kP * kRows;                      // dA accumulators
-  f32x2* x0_s = dA_s + kP * kRows;                         // saved state at the tile start
-  f32x2* a2_s = x0_s + kP * kRows;                         // A * log2(e)
-  float* dbc_s = reinterpret_cast<float*>(a2_s + kP * kRows);   // [kTB][2][kN] this tile's dB / dC sums
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* rows = smem;                                                   // [4][CR::kBytes]: u, delta, z, dout
+  f32x2* st_all = reinterpret_cast<f32x2*>(smem + 4 * CR::kBytes);     // [wave][kSub-1][kPW][64]
+  f32x4* bql = reinterpret_cast<f32x4*>(st_all + 2 * (kSub - 1) * kPW * kRows);   // [t][p]
+  float* xch = reinterpret_cast<float*>(bql + kQC);                    // [wave][64][3][kEH]
+  float* dbc = xch + 2 * kRows * 3 * kEH;                              // [kTB][2][kN]
 
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  f32x2* st = st_all + wave * (kSub - 1) * kPW * kRows;
   const int lin = xcd_remap(blockIdx.x, a.total_blocks);
   const int dblk = lin % a.nblk;
   const int bg = lin / a.nblk;
@@ -189,434 +177,453 @@ __global__ __launch_bounds__(kRows, kGrp >= 4 ? 1 : 2) void scan_bwd_kernel(cons
   const int nrows = min(kRows, H - dblk * kRows);
   const int L_ = a.seqlen;
   const bool hasZ = a.z != nullptr;
-  const bool softplus = a.softplus != 0;
+  constexpr bool softplus = kSP;
   const bool my_ok = lane < nrows;
   const int my_d = dbase + lane;
-  const int my_dc = dbase + min(lane, nrows - 1);   // lanes past the group end mirror a valid row (never stored)
+  const int my_r = min(lane, nrows - 1);      // lanes past the group end mirror a valid row (never stored)
+  const int my_dc = dbase + my_r;
 
-  // Row-block addressing.  kAligned: buffer resources (base + byte range of
-  // this wave's rows in SGPRs) and ONE 32-bit VGPR offset per access, rebuilt
-  // from an opaque lane id where used instead of being held across the pair
-  // loop; reads past a row block return 0, so ragged tails load branch-free
-  // and are masked where used.  !kAligned (odd strides): plain pointers.
-  const int64_t rows_u = (int64_t)b * a.u_bs + (int64_t)dbase * a.u_ds;
-  const int64_t rows_d = (int64_t)b * a.dt_bs + (int64_t)dbase * a.dt_ds;
-  const int64_t rows_z = hasZ ? (int64_t)b * a.z_bs + (int64_t)dbase * a.z_ds : rows_u;
-  const int64_t rows_g = (int64_t)b * a.go_bs + (int64_t)dbase * a.go_ds;
-  const TI* __restrict__ ub = reinterpret_cast<const TI*>(a.u) + rows_u;
-  const TI* __restrict__ db = reinterpret_cast<const TI*>(a.delta) + rows_d;
-  const TI* __restrict__ zb = hasZ ? reinterpret_cast<const TI*>(a.z) + rows_z : ub;
-  const TI* __restrict__ gb = reinterpret_cast<const TI*>(a.dout) + rows_g;
-  TI* __restrict__ dub = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)dbase * a.du_ds;
-  TI* __restrict__ ddb = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)dbase * a.ddt_ds;
-  TI* __restrict__ dzb = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)dbase * a.dz_ds;
-  const int64_t zds64 = hasZ ? a.z_ds : a.u_ds;
-  const TI* __restrict__ yb = hasZ ? reinterpret_cast<const TI*>(a.y) + (int64_t)b * a.y_bs + (int64_t)dbase * a.y_ds : ub;
-  const int64_t yds64 = hasZ ? a.y_ds : a.u_ds;
-  const float* __restrict__ csb = a.chunk_states + ((int64_t)b * a.dim + dbase) * a.n_states * a.dstate;
-  const uint32_t cs_ds = (uint32_t)(a.n_states * a.dstate);
-  const float* __restrict__ bcsrc = a.bct + (int64_t)bg * L_ * (2 * kN);
-  auto row_of_lane = [&]() -> uint32_t { return (uint32_t)min(opaque_lane_id(), nrows - 1); };
-  auto span = [&](int64_t ds) -> uint32_t { return (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)); };
-  const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(ub, span(a.u_ds)), rs_d = make_rsrc(db, span(a.dt_ds));
-  const __amdgpu_buffer_rsrc_t rs_z = make_rsrc(zb, span(zds64)), rs_g = make_rsrc(gb, span(a.go_ds));
-  const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(yb, span(yds64));
-  const __amdgpu_buffer_rsrc_t rs_du = make_rsrc(dub, span(a.du_ds)), rs_dd = make_rsrc(ddb, span(a.ddt_ds));
-  const __amdgpu_buffer_rsrc_t rs_dz = make_rsrc(hasZ ? (const void*)dzb : (const void*)dub, span(hasZ ? a.dz_ds : a.du_ds));
-  const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(csb, (uint32_t)nrows * cs_ds * 4u);
-  const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(bcsrc, (uint32_t)L_ * (2 * kN) * 4u);
+  // ---- the arrays this wave stages: wave 0 -> u, delta; wave 1 -> z, dout
+  const TI* src0 = reinterpret_cast<const TI*>(wave == 0 ? a.u : (hasZ ? a.z : a.dout));
+  const TI* src1 = reinterpret_cast<const TI*>(wave == 0 ? a.delta : a.dout);
+  const int64_t bs0 = wave == 0 ? a.u_bs : (hasZ ? a.z_bs : a.go_bs), ds0 = wave == 0 ? a.u_ds : (hasZ ? a.z_ds : a.go_ds);
+  const int64_t bs1 = wave == 0 ? a.dt_bs : a.go_bs, ds1 = wave == 0 ? a.dt_ds : a.go_ds;
+  const TI* rb0 = src0 + (int64_t)b * bs0 + (int64_t)dbase * ds0;
+  const TI* rb1 = src1 + (int64_t)b * bs1 + (int64_t)dbase * ds1;
+  const int slot0 = wave == 0 ? 0 : 2, slot1 = wave == 0 ? 1 : 3;
+  const bool stage0 = wave == 0 || hasZ;     // wave 1 without z stages dout only
+  auto span = [&](int64_t ds) __attribute__((always_inline)) -> uint32_t { return (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)); };
+  const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(rb0, span(ds0)), rs1 = make_rsrc(rb1, span(ds1));
+  const float* bqsrc = a.bq + (int64_t)bg * L_ * (4 * kP);
+  const __amdgpu_buffer_rsrc_t rs_bq = make_rsrc(bqsrc, (uint32_t)L_ * kP * 16u);
+  const uint32_t cs_row = (uint32_t)(a.n_states * a.dstate);   // floats per channel row of chunk states
+  const float* csb = a.chunk_states + ((int64_t)b * a.dim + dbase) * a.n_states * a.dstate;
+  const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(csb, (uint32_t)nrows * cs_row * 4u);
   const __amdgpu_buffer_rsrc_t rs_slab =
       make_rsrc(a.slab_bc + ((int64_t)bg * a.nblk + dblk) * L_ * (2 * kN), (uint32_t)L_ * (2 * kN) * 4u);
-  // one row tile of a tensor: [l0, l0 + kTB) of this lane's row
-  auto tile_in = [&](const __amdgpu_buffer_rsrc_t& rs, const TI* base, int64_t ds, int l0, bool full,
-                     uint4 (&q)[kVT]) {
-    const uint32_t rl = row_of_lane();
-    if constexpr (kAligned) {
-#pragma unroll
-      for (int k = 0; k < kVT; ++k)
-        q[k] = buf_ld16(rs, (rl * (uint32_t)ds + (uint32_t)(l0 + k * VI)) * (uint32_t)sizeof(TI));
-    } else {
-      load_row_tile<TI>(base + (int64_t)rl * ds, 0, l0, L_, full, q);
-    }
-  };
-  auto pack_tile = [&](const float (&v)[kTB], uint4 (&q)[kVT]) {
-#pragma unroll
-    for (int k = 0; k < kVT; ++k) {
-      float w[VI];
-#pragma unroll
-      for (int e = 0; e < VI; ++e) w[e] = v[k * VI + e];
-      q[k] = pack_f<TI>(w);
-    }
-  };
-  // kAligned only: store a packed row tile (positions past L masked off)
-  auto tile_out_q = [&](const __amdgpu_buffer_rsrc_t& rs, int64_t ds, uint32_t rl, int l0, bool full,
-                        const uint4 (&q)[kVT]) {
-#pragma unroll
-    for (int k = 0; k < kVT; ++k) {
-      const uint32_t off = (rl * (uint32_t)ds + (uint32_t)(l0 + k * VI)) * (uint32_t)sizeof(TI);
-      if (full) buf_st16(rs, off, q[k]);
-      else buf_st16_masked<TI>(rs, off, q[k], max(0, min(VI, L_ - (l0 + k * VI))));
-    }
-  };
-  auto tile_out = [&](const __amdgpu_buffer_rsrc_t& rs, TI* base, int64_t ds, uint32_t rl, int l0, bool full,
-                      const float (&v)[kTB]) {
-    if constexpr (kAligned) {
-      uint4 q[kVT];
-      pack_tile(v, q);
-      tile_out_q(rs, ds, rl, l0, full, q);
-    } else {
-      store_row_tile<TI>(base + (int64_t)rl * ds, 0, l0, L_, full, v);
-    }
-  };
 
-  // exact-width state rows (dstate == kN, the common case): A and the saved
-  // states move as 16-B vectors, issued back to back with one wait
-  const bool vecN = a.dstate == kN;
-  if (vecN) {
-    const f32x4* A4 = reinterpret_cast<const f32x4*>(a.A + (int64_t)my_dc * kN);
-    f32x4 av[kN / 4];
+  // ---- per-lane constants of this wave's pairs (global pair p = wave * kPW + pl)
+  f32x2 A2[kPW], hcar[kPW], dA2[kPW];
+  {
+    // unconditional loads (clamped index), masked after: no load sits behind a branch
+    const float* arow = a.A + (int64_t)my_dc * a.dstate;
+    float av[2 * kPW];
 #pragma unroll
-    for (int q = 0; q < kN / 4; ++q) av[q] = A4[q] * kLog2e;
+    for (int i = 0; i < 2 * kPW; ++i) av[i] = arow[min(2 * kPW * wave + i, a.dstate - 1)];
 #pragma unroll
-    for (int q = 0; q < kN / 4; ++q) {
-      a2_s[(2 * q) * kRows + lane] = av[q].lo;
-      a2_s[(2 * q + 1) * kRows + lane] = av[q].hi;
+    for (int pl = 0; pl < kPW; ++pl) {
+      const int n0 = 2 * (wave * kPW + pl);
+      A2[pl].x = n0 < a.dstate ? av[2 * pl] * kLog2e : 0.f;
+      A2[pl].y = n0 + 1 < a.dstate ? av[2 * pl + 1] * kLog2e : 0.f;
+      hcar[pl] = f32x2{0.f, 0.f};
+      dA2[pl] = f32x2{0.f, 0.f};
     }
-  } else {
-#pragma unroll
-    for (int p = 0; p < kP; ++p) {
-      const int n0 = 2 * p;
-      f32x2 av;
-      av.x = n0 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0] * kLog2e : 0.f;
-      av.y = n0 + 1 < a.dstate ? a.A[(int64_t)my_dc * a.dstate + n0 + 1] * kLog2e : 0.f;
-      a2_s[p * kRows + lane] = av;
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < kP; ++p) {
-    carry_s[p * kRows + lane] = f32x2{0.f, 0.f};
-    dA_s[p * kRows + lane] = f32x2{0.f, 0.f};
   }
   const float Dv = a.D ? a.D[my_dc] : 0.f;
   const float biasv = a.delta_bias ? a.delta_bias[my_dc] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
 
-  // ---- prefetch registers: one tile's rows, B/C quads and saved start
-  // state.  Tiles are walked last to first, so only the first tile visited can
-  // be ragged: every prefetch inside the loop is a full tile and (kAligned)
-  // compiles to unconditional 16-B loads -- no control flow around the loads,
-  // so nothing forces a vmcnt wait before the loads are consumed a tile later.
-  uint4 ru[kVT], rd[kVT], rz[kVT], rg[kVT];
-  // 16-bit inputs: rows are fetched for a GROUP of kG tiles at a time (the
-  // loads go out back to back, so each 128-B line a lane touches is fetched
-  // once per 8 kG positions instead of once per 8); the later tiles of the
-  // group wait in su.. (kG = 4 runs at one wave per SIMD for the registers)
-  constexpr int kG = (kAligned && sizeof(TI) == 2) ? kGrp : 1;
-  constexpr int kS = kG > 1 ? kG - 1 : 1;
-  uint4 su[kS][kVT], sd[kS][kVT], sz[kS][kVT], sg[kS][kVT];
-  f32x4 pbc[kBCPer];
-  f32x4 px0[kN / 4];
-  auto load_rows = [&](int ti, bool full, uint4 (&qu)[kVT], uint4 (&qd)[kVT], uint4 (&qz)[kVT], uint4 (&qg)[kVT]) {
-    const int l0 = ti * kTB;
-    tile_in(rs_u, ub, a.u_ds, l0, full, qu);
-    tile_in(rs_d, db, a.dt_ds, l0, full, qd);
-    tile_in(rs_z, zb, zds64, l0, full, qz);     // (no z: a harmless re-read of u, no branch)
-    tile_in(rs_g, gb, a.go_ds, l0, full, qg);
-  };
-  auto prefetch_bc = [&](int ti) {
-    const int l0 = ti * kTB;
+  // ---- prefetch registers: this wave's two row arrays of one chunk, its share
+  // of the chunk's B/C quads, and the saved state at the chunk start (own pairs)
+  uint4 pf0[VPR], pf1[VPR];
+  f32x4 pq[kQPer];
+  f32x4 px0[kPW / 2];
+  auto prefetch = [&](int c) __attribute__((always_inline)) {
+    const int l0 = c * kTC;
+    const bool valid = c >= 0;
 #pragma unroll
-    for (int k = 0; k < kBCPer; ++k) {       // quad q = lane + 64 k -> (pair q / kTB, position q % kTB)
-      const int q = lane + k * kRows;
-      const int pp = min(q / kTB, kP - 1), t = q % kTB;
-      // positions past L read as 0 (buffer range); quads q >= kBCQ are never stored
-      const uint32_t off = (uint32_t)(((l0 + t) * (2 * kN) + 2 * pp) * 4);
-      const uint2 bb = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_bc, off, 0, 0));
-      const uint2 cc = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_bc, off + kN * 4, 0, 0));
-      pbc[k] = f32x4{__uint_as_float(bb.x), __uint_as_float(bb.y), __uint_as_float(cc.x), __uint_as_float(cc.y)};
-    }
-  };
-  // saved state at the start of tile ti (zero for ti == 0): the row's first
-  // kN floats as kN/4 16-B loads (dword-aligned for any dstate; entries past
-  // dstate are masked where consumed).  Unconditional: tile 0 gets an offset
-  // past the buffer range, which reads 0.  Neither a select on the loaded data
-  // nor a branch around the loads may appear here -- either makes the compiler
-  // wait for them (and for every older load and store) on the spot.
-  auto prefetch_x0 = [&](int ti) {
-    const uint32_t off = ti > 0 ? (row_of_lane() * cs_ds + (uint32_t)((ti - 1) * a.dstate)) * 4u : 0x80000000u;
-#pragma unroll
-    for (int q = 0; q < kN / 4; ++q) px0[q] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, off + 16 * q));
-  };
-
-#ifdef MC_BWD_STAMPS
-  uint64_t st_pro = 0, st_pair = 0, st_out = 0;
-#endif
-  const int ntiles = (L_ + kTB - 1) / kTB;
-  // mode -1: one tile at a time; m >= 0: the m-th tile (from the top) of a group
-  auto tile_body = [&](const int ti, auto mode_c) {
-    constexpr int kMode = decltype(mode_c)::value;
-#ifdef MC_BWD_STAMPS
-    const uint64_t s0 = __builtin_amdgcn_s_memtime();
-#endif
-    const int l0 = ti * kTB;
-    const bool full = kAligned && (l0 + kTB <= L_);
-    wave_lds_sync();                             // previous tile is done with the B/C quads
-#pragma unroll
-    for (int k = 0; k < kBCPer; ++k) {
-      const int q = lane + k * kRows;
-      if ((k + 1) * kRows <= kBCQ || q < kBCQ) bcq[q] = pbc[k];
-    }
-    // this tile's per-position scalars (from the prefetched raw rows)
-    float dt[kTB], dtu[kTB], gy[kTB];
-#pragma unroll
-    for (int t = 0; t < kTB; ++t) {
-      // positions past L (ragged first tile) hold whatever the 16-B loads
-      // returned: zero them before they meet the recurrence
-      const bool tv = full || l0 + t < L_;
-      const float uv = tv ? elem_f<TI>(ru[t / VI], t % VI) : 0.f;
-      const float r = elem_f<TI>(rd[t / VI], t % VI) + biasv;
-      const float go = tv ? elem_f<TI>(rg[t / VI], t % VI) : 0.f;
-      float d = softplus ? softplus_f(r) : r;
-      d = tv ? d : 0.f;
-      dt[t] = d;
-      // lanes mirroring a row past the group end: dtu = gy = 0 zeroes their
-      // dB / dC contributions here, once per tile, instead of a select per
-      // value in every pair's reductions (their own outputs are never stored)
-      dtu[t] = my_ok ? d * uv : 0.f;
-      if (hasZ) {
-        const float zv = tv ? elem_f<TI>(rz[t / VI], t % VI) : 0.f;
-        gy[t] = my_ok ? go * zv * sigmoid_f(zv) : 0.f;   // dout * silu(z)
+    for (int k = 0; k < VPR; ++k) {
+      const int j = lane + k * kRows;
+      const int r = min(j / VPR, nrows - 1), cc = j % VPR;
+      const int col0 = l0 + cc * VI;
+      if constexpr (kAligned) {
+        // chunk -1: an offset past every buffer range reads 0 (no branch around the loads)
+        const uint32_t o0 = valid ? (uint32_t)(r * ds0 + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
+        const uint32_t o1 = valid ? (uint32_t)(r * ds1 + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
+        pf0[k] = buf_ld16(rs0, o0);
+        pf1[k] = buf_ld16(rs1, o1);
       } else {
-        gy[t] = my_ok ? go : 0.f;
+        const int nv = valid ? max(0, min(VI, L_ - col0)) : 0;
+        pf0[k] = ld16_masked(rb0 + (int64_t)r * ds0 + (valid ? col0 : 0), nv);
+        pf1[k] = ld16_masked(rb1 + (int64_t)r * ds1 + (valid ? col0 : 0), nv);
       }
     }
-    // saved state at the tile start -> LDS
 #pragma unroll
-    for (int q = 0; q < kN / 4; ++q) {
-      const f32x4 v = px0[q];
-      x0_s[(2 * q) * kRows + lane] = f32x2{4 * q < a.dstate ? v.x : 0.f, 4 * q + 1 < a.dstate ? v.y : 0.f};
-      x0_s[(2 * q + 1) * kRows + lane] = f32x2{4 * q + 2 < a.dstate ? v.z : 0.f, 4 * q + 3 < a.dstate ? v.w : 0.f};
+    for (int k = 0; k < kQPer; ++k) {
+      const int q = tid + k * kWG;
+      const uint32_t o = valid && q < kQC ? (uint32_t)((l0 * kP + q) * 16) : 0x80000000u;
+      pq[k] = __builtin_bit_cast(f32x4, buf_ld16(rs_bq, o));
     }
-    wave_lds_sync();                             // B/C quads staged
-    // next tile's loads fly under this tile's math.  kAligned: unconditional
-    // (tile -1 addresses land outside the buffers or in unused row bytes)
-    if constexpr (kMode < 0) {
-      if (kAligned || ti > 0) load_rows(ti - 1, kAligned, ru, rd, rz, rg);
-    } else if constexpr (kMode < kG - 1) {     // next tile of the group is already here
+    // saved state after chunk c-1 (zero for c == 0): floats [2 kPW wave, 2 kPW (wave+1)) of my row
+    const uint32_t ox = c > 0 ? ((uint32_t)my_r * cs_row + (uint32_t)((c - 1) * a.dstate + 2 * kPW * wave)) * 4u
+                              : 0x80000000u;
+#pragma unroll
+    for (int k = 0; k < kPW / 2; ++k) px0[k] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox + 16 * k));
+  };
+
+  auto own_vec = [&](int slot, int blk) __attribute__((always_inline)) -> uint4 {   // this lane's row, 16-B block blk of the chunk
+    return *reinterpret_cast<const uint4*>(rows + slot * CR::kBytes + CR::off(lane, blk));
+  };
+
+  const int nch = (L_ + kTC - 1) / kTC;
+  prefetch(nch - 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+
+  for (int c = nch - 1; c >= 0; --c) {
+    const int l0 = c * kTC;
+    // ---- stage the prefetched rows and quads, take the chunk-start state
+#pragma unroll
+    for (int k = 0; k < VPR; ++k) {
+      const int j = lane + k * kRows;
+      const int off = CR::off(j / VPR, j % VPR);
+      if (stage0) *reinterpret_cast<uint4*>(rows + slot0 * CR::kBytes + off) = pf0[k];
+      *reinterpret_cast<uint4*>(rows + slot1 * CR::kBytes + off) = pf1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kQPer; ++k) {
+      const int q = tid + k * kWG;
+      if ((k + 1) * kWG <= kQC || q < kQC) bql[q] = pq[k];
+    }
+    f32x2 x0r[kPW];
+#pragma unroll
+    for (int k = 0; k < kPW / 2; ++k) {
+      const int n0 = 2 * kPW * wave + 4 * k;
+      const f32x4 v = px0[k];
+      x0r[2 * k] = f32x2{n0 < a.dstate ? v.x : 0.f, n0 + 1 < a.dstate ? v.y : 0.f};
+      x0r[2 * k + 1] = f32x2{n0 + 2 < a.dstate ? v.z : 0.f, n0 + 3 < a.dstate ? v.w : 0.f};
+    }
+    lds_barrier();
+    prefetch(c - 1);     // flies under this chunk's math
+
+    const int nsub = min(kSub, (L_ - l0 + kTB - 1) / kTB);   // sub-tiles holding positions < L
+
+    // per-position scalars of sub-tile s from the staged rows (positions >= L zeroed)
+    auto sub_scalars = [&](int s, float (&dt)[kTB], float (&dtu)[kTB], float (&gy)[kTB], bool want_gy) {
+      uint4 qu[kVT], qd[kVT], qz[kVT], qg[kVT];
 #pragma unroll
       for (int k = 0; k < kVT; ++k) {
-        ru[k] = su[kMode][k]; rd[k] = sd[kMode][k]; rz[k] = sz[kMode][k]; rg[k] = sg[kMode][k];
+        qu[k] = own_vec(0, s * kVT + k);
+        qd[k] = own_vec(1, s * kVT + k);
+        if (want_gy) {
+          qz[k] = own_vec(2, s * kVT + k);
+          qg[k] = own_vec(3, s * kVT + k);
+        }
       }
-    } else {                                   // last tile of the group: fetch the next group
-      load_rows(ti - 1, true, ru, rd, rz, rg);   // (tiles below 0 land outside the buffers
-#pragma unroll                                 //  or in unused row bytes)
-      for (int j = 0; j < kG - 1; ++j) load_rows(ti - 2 - j, true, su[j], sd[j], sz[j], sg[j]);
-    }
-    prefetch_bc(ti - 1);
-    prefetch_x0(ti - 1);
-    // the forward's pre-gate y of this tile (dz only), consumed after the pair loop
-    uint4 cy[kVT];
-    tile_in(rs_y, yb, yds64, l0, full, cy);
-
-    f32x2 S2[kTB], Q2[kTB];
-#pragma unroll
-    for (int t = 0; t < kTB; ++t) { S2[t] = f32x2{0.f, 0.f}; Q2[t] = f32x2{0.f, 0.f}; }
-
-#ifdef MC_BWD_STAMPS
-    const uint64_t s1 = __builtin_amdgcn_s_memtime();
-    st_pro += s1 - s0;
-#endif
-#pragma unroll 1
-    for (int p = 0; p < kP; ++p) {
-      const f32x2 A2p = a2_s[p * kRows + lane];
-      f32x4 bc[kTB];
-#pragma unroll
-      for (int t = 0; t < kTB; ++t) bc[t] = bcq[p * kTB + t];
-      // forward sweep: states and decays of this pair over the tile
-      f32x2 xs[kTB], as[kTB];
-      const f32x2 x0p = x0_s[p * kRows + lane];
-      f32x2 x = x0p;
 #pragma unroll
       for (int t = 0; t < kTB; ++t) {
-        const f32x2 arg = A2p * dt[t];
-#ifdef MC_DIAG_NOEXP
-        const f32x2 aa = arg;
-#else
-        const f32x2 aa = {fast_exp2(arg.x), fast_exp2(arg.y)};
-#endif
-        x = aa * x + bc[t].lo * dtu[t];
-        xs[t] = x;
-        as[t] = aa;
+        const bool tv = l0 + s * kTB + t < L_;
+        const float uv = tv ? elem_f<TI>(qu[t / VI], t % VI) : 0.f;
+        const float r = elem_f<TI>(qd[t / VI], t % VI) + biasv;
+        float d = softplus ? softplus_f(r) : r;
+        d = tv ? d : 0.f;
+        dt[t] = d;
+        // lanes mirroring a row past the group end: dtu = gy = 0 zeroes their dB / dC terms
+        dtu[t] = my_ok ? d * uv : 0.f;
+        if (want_gy) {
+          const float go = tv ? elem_f<TI>(qg[t / VI], t % VI) : 0.f;
+          float gyv = go;
+          if (hasZ) {
+            const float zv = tv ? elem_f<TI>(qz[t / VI], t % VI) : 0.f;
+            gyv = go * zv * sigmoid_f(zv);   // dout * silu(z)
+          }
+          gy[t] = my_ok ? gyv : 0.f;
+        }
       }
-      // dC_t,n = sum over the wave's channels of gy_t x_t,n
-      {
-        float red[2 * kTB];
+    };
+
+    // ---- recompute the states at the starts of sub-tiles 1 .. nsub-1 (own pairs) -> LDS
+    {
+      f32x2 x[kPW];
+#pragma unroll
+      for (int pl = 0; pl < kPW; ++pl) x[pl] = x0r[pl];
+#pragma unroll 1
+      for (int s = 0; s + 1 < nsub; ++s) {
+        float dt[kTB], dtu[kTB], gy[kTB];
+        sub_scalars(s, dt, dtu, gy, false);
 #pragma unroll
         for (int t = 0; t < kTB; ++t) {
-          const f32x2 v = xs[t] * gy[t];
-          red[2 * t] = v.x;
-          red[2 * t + 1] = v.y;
+          if (t % 2 == 0) __builtin_amdgcn_sched_barrier(0);   // bounded hoisting: 2 positions x kPW pairs
+#pragma unroll
+          for (int pl = 0; pl < kPW; ++pl) {
+            const f32x2 bb = reinterpret_cast<const f32x2*>(bql + (s * kTB + t) * kP + wave * kPW + pl)[0];
+            const f32x2 arg = A2[pl] * dt[t];
+            const f32x2 aa = {fast_exp2(arg.x), fast_exp2(arg.y)};
+            x[pl] = aa * x[pl] + bb * dtu[t];
+          }
         }
-#ifdef MC_DIAG_NORED
-        float tot = 0.f;
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 2 * kTB; ++i) tot += red[i];
-#else
-        const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
-#endif
-        const int j = lane / (64 / (2 * kTB));
-        const int t = j / 2, n = 2 * p + (j & 1);
-        if ((lane & (64 / (2 * kTB) - 1)) == 0)
-          dbc_s[(t * 2 + 1) * kN + n] = tot;
-      }
-      // reverse sweep: adjoint of the state.  The B/C quads are read from LDS
-      // again (the compiler barrier stops them being kept live across the dC
-      // reduction: 32 VGPRs at the kernel's pressure peak)
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int t = 0; t < kTB; ++t) bc[t] = bcq[p * kTB + t];
-      f32x2 h = carry_s[p * kRows + lane];
-      f32x2 dAp = dA_s[p * kRows + lane];
-      float red[2 * kTB];
-#pragma unroll
-      for (int t = kTB - 1; t >= 0; --t) {
-        h = bc[t].hi * gy[t] + h;                  // + C_t gy_t
-        S2[t] = h * bc[t].lo + S2[t];
-        const f32x2 vb = h * dtu[t];
-        red[2 * t] = vb.x;
-        red[2 * t + 1] = vb.y;
-        const f32x2 ha = h * as[t];
-        const f32x2 hax = ha * (t > 0 ? xs[t - 1] : x0p);
-        Q2[t] = hax * A2p + Q2[t];
-        dAp = hax * dt[t] + dAp;
-        h = ha;
-      }
-      carry_s[p * kRows + lane] = h;
-      dA_s[p * kRows + lane] = dAp;
-      {
-#ifdef MC_DIAG_NORED
-        float tot = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2 * kTB; ++i) tot += red[i];
-#else
-        const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
-#endif
-        const int j = lane / (64 / (2 * kTB));
-        const int t = j / 2, n = 2 * p + (j & 1);
-        if ((lane & (64 / (2 * kTB) - 1)) == 0)
-          dbc_s[(t * 2 + 0) * kN + n] = tot;
+        for (int pl = 0; pl < kPW; ++pl) st[(s * kPW + pl) * kRows + lane] = x[pl];
       }
     }
 
-#ifdef MC_BWD_STAMPS
-    const uint64_t s2 = __builtin_amdgcn_s_memtime();
-    st_pair += s2 - s1;
-#endif
-    // ---- the tile's dB / dC sums: one coalesced 16-B store per lane into
-    // this wave's slab block (positions past L fall outside the buffer range
-    // and are dropped)
-    wave_lds_sync();
+    // ---- sub-tiles in reverse
+#pragma unroll 1
+    for (int s = nsub - 1; s >= 0; --s) {
+      float dt[kTB], dtu[kTB], gy[kTB];
+      sub_scalars(s, dt, dtu, gy, true);
+      float Sa[kTB], Qa[kTB], Ya[kTB];      // per-position sums over this wave's pairs
 #pragma unroll
-    for (int k = 0; k < (kTB * 2 * kN) / (4 * kRows) + ((kTB * 2 * kN) % (4 * kRows) ? 1 : 0); ++k) {
-      const int f = 4 * (lane + k * kRows);
-      if (f < kTB * 2 * kN) {
-        const uint4 v = *reinterpret_cast<const uint4*>(dbc_s + f);
-        buf_st16(rs_slab, (uint32_t)((l0 * 2 * kN + f) * 4), v);
-      }
-    }
-    // ---- per-position outputs of my channel (this tile's rows re-read: L2
-    // hits; keeping them in registers through the pair loop would spill)
-    uint4 cu[kVT], cd[kVT], cz[kVT], cg[kVT];
-    tile_in(rs_u, ub, a.u_ds, l0, full, cu);
-    tile_in(rs_d, db, a.dt_ds, l0, full, cd);
-    tile_in(rs_z, zb, zds64, l0, full, cz);
-    tile_in(rs_g, gb, a.go_ds, l0, full, cg);
-    float o_du[kTB], o_dd[kTB], o_dz[kTB];
-#pragma unroll
-    for (int t = 0; t < kTB; ++t) {
-      const float uv = elem_f<TI>(cu[t / VI], t % VI);
-      const float r = elem_f<TI>(cd[t / VI], t % VI) + biasv;
-      const float go = elem_f<TI>(cg[t / VI], t % VI);
-      const float S = S2[t].x + S2[t].y;
-      const float Q = (Q2[t].x + Q2[t].y) * kLn2;   // A2 carries log2(e)
-      const float sg = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
-      float gyv = go;
-      float gz = 0.f;
-      if (hasZ) {
-        const float zv = elem_f<TI>(cz[t / VI], t % VI);
-        const float sgz = sigmoid_f(zv);
-        gyv = go * zv * sgz;
-        gz = go * sgz * (1.f + zv * (1.f - sgz));
-      }
-      o_dz[t] = gz * elem_f<TI>(cy[t / VI], t % VI);   // y + D u, as the forward produced it
-      o_du[t] = fmaf(Dv, gyv, dt[t] * S);
-      const float dr = fmaf(uv, S, Q) * sg;
-      o_dd[t] = dr;
-      if (l0 + t < L_ && my_ok) {
-        dDacc = fmaf(gyv, uv, dDacc);
-        dbacc += dr;
-      }
-    }
-    if (my_ok) {
-      const uint32_t rl = row_of_lane();
-      tile_out(rs_du, dub, a.du_ds, rl, l0, full, o_du);
-      tile_out(rs_dd, ddb, a.ddt_ds, rl, l0, full, o_dd);
-      if (hasZ) tile_out(rs_dz, dzb, a.dz_ds, rl, l0, full, o_dz);
-    }
-#ifdef MC_BWD_STAMPS
-    st_out += __builtin_amdgcn_s_memtime() - s2;
-#endif
-  };
+      for (int t = 0; t < kTB; ++t) { Sa[t] = Qa[t] = Ya[t] = 0.f; }
 
-  // drain once before the loop: the loop header then merges "nothing pending"
-  // from the entry edge, so consuming a prefetch never waits for the previous
-  // tile's stores (vmcnt counts stores too on gfx9)
-  if constexpr (kG > 1) {
-    const int ngroups = (ntiles + kG - 1) / kG;   // a partial group adds tiles past L (fully masked)
-    const int top = kG * ngroups - 1;
-    load_rows(top, true, ru, rd, rz, rg);
 #pragma unroll
-    for (int j = 0; j < kG - 1; ++j) load_rows(top - 1 - j, true, su[j], sd[j], sz[j], sg[j]);
-    prefetch_bc(top);
-    prefetch_x0(top);
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int k = ngroups - 1; k >= 0; --k) {
-      const int t0 = kG * k + kG - 1;
-      tile_body(t0, std::integral_constant<int, 0>());
-      if constexpr (kG >= 2) tile_body(t0 - 1, std::integral_constant<int, 1>());
-      if constexpr (kG >= 3) tile_body(t0 - 2, std::integral_constant<int, 2>());
-      if constexpr (kG >= 4) tile_body(t0 - 3, std::integral_constant<int, 3>());
+      for (int pl = 0; pl < kPW; ++pl) {
+        __builtin_amdgcn_sched_barrier(0);      // one pair at a time: bounded register live ranges
+        const int p = wave * kPW + pl;
+        // Pin the program order of the pairs: empty volatile asm statements keep their
+        // order, and this pair's inputs / last pair's outputs pass through them, so the
+        // instruction-selection DAG cannot run all forward sweeps ahead of the reverse
+        // sweeps (that interleaving keeps every pair's xs / as live at once).
+        f32x2 a2p = A2[pl];
+        asm volatile("" : "+v"(a2p));
+        const f32x2 x0p = s == 0 ? x0r[pl] : st[((s - 1) * kPW + pl) * kRows + lane];
+        // forward sweep: states and decays of this pair over the sub-tile (B halves only)
+        f32x2 xs[kTB], as[kTB];
+        // the decays first (independent of the state chain), then the chain itself
+#pragma unroll
+        for (int t = 0; t < kTB; ++t) {
+          const f32x2 arg = a2p * dt[t];
+          as[t] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+        }
+        f32x2 x = x0p;
+#pragma unroll
+        for (int t = 0; t < kTB; ++t) {
+          const f32x2 bb = reinterpret_cast<const f32x2*>(bql + (s * kTB + t) * kP + p)[0];
+          x = as[t] * x + bb * dtu[t];
+          xs[t] = x;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // dC_t,n = sum over the wave's channels of gy_t x_t,n
+        {
+          float red[2 * kTB];
+#pragma unroll
+          for (int t = 0; t < kTB; ++t) {
+            const f32x2 v = xs[t] * gy[t];
+            red[2 * t] = v.x;
+            red[2 * t + 1] = v.y;
+          }
+          const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+          const int j = lane / (64 / (2 * kTB));
+          if ((lane & (64 / (2 * kTB) - 1)) == 0) dbc[((j >> 1) * 2 + 1) * kN + 2 * p + (j & 1)] = tot;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // reverse sweep: adjoint of the state (+ y_t = sum_n C x for dz)
+        f32x2 h = hcar[pl];
+        f32x2 dAp = dA2[pl];
+        float red[2 * kTB];
+        // quads read one position ahead of their use (LDS latency under the chain)
+        f32x4 qn = bql[(s * kTB + kTB - 1) * kP + p];
+#pragma unroll
+        for (int t = kTB - 1; t >= 0; --t) {
+          const f32x4 q = qn;
+          if (t > 0) qn = bql[(s * kTB + t - 1) * kP + p];
+          Ya[t] = fmaf(q.hi.x, xs[t].x, fmaf(q.hi.y, xs[t].y, Ya[t]));
+          h = q.hi * gy[t] + h;                     // + C_t gy_t
+          Sa[t] = fmaf(h.x, q.lo.x, fmaf(h.y, q.lo.y, Sa[t]));
+          const f32x2 vb = h * dtu[t];
+          red[2 * t] = vb.x;
+          red[2 * t + 1] = vb.y;
+          const f32x2 ha = h * as[t];
+          const f32x2 hax = ha * (t > 0 ? xs[t - 1] : x0p);
+          const f32x2 qa = hax * a2p;
+          Qa[t] += qa.x + qa.y;
+          dAp = hax * dt[t] + dAp;
+          h = ha;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+v"(h), "+v"(dAp));
+#pragma unroll
+        for (int t = 0; t < kTB; ++t) asm volatile("" : "+v"(Sa[t]), "+v"(Qa[t]), "+v"(Ya[t]));
+        hcar[pl] = h;
+        dA2[pl] = dAp;
+        {
+          const float tot = wave_transpose_reduce<2 * kTB>(red, lane);
+          const int j = lane / (64 / (2 * kTB));
+          if ((lane & (64 / (2 * kTB) - 1)) == 0) dbc[((j >> 1) * 2 + 0) * kN + 2 * p + (j & 1)] = tot;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+
+      // ---- exchange partial sums, then each wave finishes half of the sub-tile's positions.
+      // The wave index is made a compile-time constant here so that every register
+      // array (Sa / Qa / Ya / dt) is indexed statically (a runtime index would
+      // demote them to scratch).
+      auto exchange_and_finish = [&](auto wc) __attribute__((always_inline)) {
+        constexpr int W = decltype(wc)::value;
+        {   // the other wave finishes positions [kEH*(1-W), +kEH): give it my partial sums
+          constexpr int t0 = kEH * (1 - W);
+          float* xo = xch + (W * kRows + lane) * 3 * kEH;
+          f32x4 sv, qv, yv;
+#pragma unroll
+          for (int e = 0; e < kEH; ++e) { sv[e] = Sa[t0 + e]; qv[e] = Qa[t0 + e]; yv[e] = Ya[t0 + e]; }
+          reinterpret_cast<f32x4*>(xo)[0] = sv;
+          reinterpret_cast<f32x4*>(xo)[1] = qv;
+          reinterpret_cast<f32x4*>(xo)[2] = yv;
+        }
+        lds_barrier();
+        // my positions t = kEH*W + e: du, ddelta, dz written over the consumed rows
+        constexpr int t0 = kEH * W;
+        const float* xi = xch + ((1 - W) * kRows + lane) * 3 * kEH;
+        const f32x4 so = reinterpret_cast<const f32x4*>(xi)[0];
+        const f32x4 qo = reinterpret_cast<const f32x4*>(xi)[1];
+        const f32x4 yo = reinterpret_cast<const f32x4*>(xi)[2];
+        const int blk = s * kVT + t0 / VI;            // 16-B block holding my positions
+        constexpr int eo = t0 % VI;                   // first element of mine inside it
+        const uint4 qu = own_vec(0, blk), qd = own_vec(1, blk), qz = own_vec(2, blk), qg = own_vec(3, blk);
+        float o_du[kEH], o_dd[kEH], o_dz[kEH];
+#pragma unroll
+        for (int e = 0; e < kEH; ++e) {
+          const int t = t0 + e;
+          const bool tv = l0 + s * kTB + t < L_;
+          const float uv = tv ? elem_f<TI>(qu, eo + e) : 0.f;
+          const float r = elem_f<TI>(qd, eo + e) + biasv;
+          const float go = tv ? elem_f<TI>(qg, eo + e) : 0.f;
+          const float S = Sa[t] + so[e];
+          const float Q = (Qa[t] + qo[e]) * kLn2;   // A2 carries log2(e)
+          const float Y = Ya[t] + yo[e];
+          const float sg = softplus ? (r > 20.f ? 1.f : sigmoid_f(r)) : 1.f;
+          float gyv = go, gz = 0.f;
+          if (hasZ) {
+            const float zv = tv ? elem_f<TI>(qz, eo + e) : 0.f;
+            const float sgz = sigmoid_f(zv);
+            gyv = go * zv * sgz;
+            gz = go * sgz * (1.f + zv * (1.f - sgz));
+          }
+          o_dz[e] = gz * fmaf(Dv, uv, Y);             // dout * silu'(z) * (y + D u)
+          o_du[e] = fmaf(Dv, gyv, dt[t] * S);
+          const float dr = fmaf(uv, S, Q) * sg;
+          o_dd[e] = dr;
+          if (tv && my_ok) {
+            dDacc = fmaf(gyv, uv, dDacc);
+            dbacc += dr;
+          }
+        }
+        // write over the consumed row bytes (read above by this lane only)
+        auto put = [&](int slot, const float (&v)[kEH]) {
+          char* dst = rows + slot * CR::kBytes + CR::off(lane, blk) + eo * (int)sizeof(TI);
+          if constexpr (sizeof(TI) == 4) {
+            *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            *reinterpret_cast<uint2*>(dst) = make_uint2(bits16<TI>(v[0]) | (bits16<TI>(v[1]) << 16),
+                                                        bits16<TI>(v[2]) | (bits16<TI>(v[3]) << 16));
+          }
+        };
+        put(0, o_du);
+        put(1, o_dd);
+        if (hasZ) put(2, o_dz);
+      };
+      if (wave == 0) exchange_and_finish(std::integral_constant<int, 0>());
+      else exchange_and_finish(std::integral_constant<int, 1>());
+      // ---- the sub-tile's dB / dC sums -> this workgroup's slab (positions past L dropped)
+      if (wave == 0) {
+        constexpr int kF = kTB * 2 * kN;   // floats
+#pragma unroll
+        for (int k = 0; k < (kF + 4 * kRows - 1) / (4 * kRows); ++k) {
+          const int f = 4 * (lane + k * kRows);
+          if (f < kF) {
+            const uint4 v = *reinterpret_cast<const uint4*>(dbc + f);
+            buf_st16(rs_slab, (uint32_t)(((l0 + s * kTB) * 2 * kN + f) * 4), v);
+          }
+        }
+      }
+      lds_barrier();
     }
-  } else {
-    load_rows(ntiles - 1, kAligned && ntiles * kTB <= L_, ru, rd, rz, rg);
-    prefetch_bc(ntiles - 1);
-    prefetch_x0(ntiles - 1);
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int ti = ntiles - 1; ti >= 0; --ti) tile_body(ti, std::integral_constant<int, -1>());
+
+    // ---- the chunk's du / ddelta (wave 0) and dz (wave 1): coalesced 16-B stores
+    {
+      const int nst = wave == 0 ? 2 : (hasZ ? 1 : 0);
+      for (int sidx = 0; sidx < nst; ++sidx) {
+        const int slot = wave == 0 ? sidx : 2;
+        TI* base;
+        int64_t ds;
+        if (slot == 0) { base = reinterpret_cast<TI*>(a.du) + (int64_t)b * a.du_bs + (int64_t)dbase * a.du_ds; ds = a.du_ds; }
+        else if (slot == 1) { base = reinterpret_cast<TI*>(a.ddelta) + (int64_t)b * a.ddt_bs + (int64_t)dbase * a.ddt_ds; ds = a.ddt_ds; }
+        else { base = reinterpret_cast<TI*>(a.dz) + (int64_t)b * a.dz_bs + (int64_t)dbase * a.dz_ds; ds = a.dz_ds; }
+        const __amdgpu_buffer_rsrc_t rso = make_rsrc(base, span(ds));
+#pragma unroll
+        for (int k = 0; k < VPR; ++k) {
+          const int j = lane + k * kRows;
+          const int r = j / VPR, cc = j % VPR;
+          const int col0 = l0 + cc * VI;
+          if (r < nrows && col0 < L_) {
+            const uint4 v = *reinterpret_cast<const uint4*>(rows + slot * CR::kBytes + CR::off(r, cc));
+            const int nv = min(VI, L_ - col0);
+            if constexpr (kAligned) {
+              const uint32_t o = (uint32_t)(r * ds + col0) * (uint32_t)sizeof(TI);
+              if (nv == VI) buf_st16(rso, o, v);
+              else buf_st16_masked<TI>(rso, o, v, nv);
+            } else {
+              st16_masked(base + (int64_t)r * ds + col0, v, nv);
+            }
+          }
+        }
+      }
+    }
+    lds_barrier();    // rows are free for the next chunk's staging
   }
-#ifdef MC_BWD_STAMPS
-  // diagnostic build: per-wave segment cycles -> slab_d (outputs are invalid in this build)
-  if (lane == 0) {
-    uint64_t* dbg = reinterpret_cast<uint64_t*>(a.slab_d) + (int64_t)blockIdx.x * 4;
-    dbg[0] = st_pro; dbg[1] = st_pair; dbg[2] = st_out; dbg[3] = ntiles;
-  }
-  return;
-#endif
 
+  // ---- per-channel parameter gradients: dA (each wave its pairs), dD / dbias (both waves' halves)
   if (my_ok) {
-    // slab_a is [b][n][d]: coalesced along d
 #pragma unroll
-    for (int p = 0; p < kP; ++p) {
-      const f32x2 v = dA_s[p * kRows + lane];
-      a.slab_a[((int64_t)b * kN + 2 * p) * a.dim + my_d] = v.x;
-      a.slab_a[((int64_t)b * kN + 2 * p + 1) * a.dim + my_d] = v.y;
+    for (int pl = 0; pl < kPW; ++pl) {
+      const int n0 = 2 * (wave * kPW + pl);
+      a.slab_a[((int64_t)b * kN + n0) * a.dim + my_d] = dA2[pl].x;
+      a.slab_a[((int64_t)b * kN + n0 + 1) * a.dim + my_d] = dA2[pl].y;
     }
-    a.slab_d[(int64_t)b * a.dim + my_d] = dDacc;
-    a.slab_bias[(int64_t)b * a.dim + my_d] = dbacc;
+  }
+  if (wave == 1) { xch[2 * lane] = dDacc; xch[2 * lane + 1] = dbacc; }
+  lds_barrier();
+  if (wave == 0 && my_ok) {
+    a.slab_d[(int64_t)b * a.dim + my_d] = dDacc + xch[2 * lane];
+    a.slab_bias[(int64_t)b * a.dim + my_d] = dbacc + xch[2 * lane + 1];
   }
 }
 
-// dB / dC: sum the per-wave slabs; dA / dD / dbias: sum the per-batch slabs.
+// B/C as the backward consumes them: fp32 quads {B_n, B_n+1, C_n, C_n+1} per
+// (b, g, l, pair), states >= dstate zero.  One thread per quad.
+template <typename TW, int kN>
+__global__ __launch_bounds__(256) void bc_quad_kernel(const TW* __restrict__ B, const TW* __restrict__ C,
+                                                      int64_t B_bs, int64_t B_gs, int64_t B_ns, int64_t C_bs,
+                                                      int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
+                                                      f32x4* __restrict__ out) {
+  constexpr int kP = kN / 2;
+  const int64_t total = (int64_t)batch * G * L * kP;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i % kP);
+    const int64_t rest = i / kP;
+    const int l = (int)(rest % L);
+    const int64_t bg = rest / L;
+    const int gg = (int)(bg % G), bb = (int)(bg / G);
+    const TW* bs = B + (int64_t)bb * B_bs + (int64_t)gg * B_gs + l;
+    const TW* cs = C + (int64_t)bb * C_bs + (int64_t)gg * C_gs + l;
+    const int n0 = 2 * p;
+    f32x4 v;
+    v.x = n0 < dstate ? to_f(bs[(int64_t)n0 * B_ns]) : 0.f;
+    v.y = n0 + 1 < dstate ? to_f(bs[(int64_t)(n0 + 1) * B_ns]) : 0.f;
+    v.z = n0 < dstate ? to_f(cs[(int64_t)n0 * C_ns]) : 0.f;
+    v.w = n0 + 1 < dstate ? to_f(cs[(int64_t)(n0 + 1) * C_ns]) : 0.f;
+    out[i] = v;
+  }
+}
+
+template <typename TW>
+static hipError_t launch_bc_quads(const mc_scan_bwd_params* p, int np, f32x4* out, hipStream_t s) {
+  const int64_t total = (int64_t)p->batch * p->n_groups * p->seqlen * (np / 2);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  const TW* B = reinterpret_cast<const TW*>(p->B);
+  const TW* C = reinterpret_cast<const TW*>(p->C);
+#define MC_BCQ(NP)                                                                                                 \
+  hipLaunchKernelGGL((bc_quad_kernel<TW, NP>), grid, 256, 0, s, B, C, p->B_batch_stride, p->B_group_stride,       \
+                     p->B_dstate_stride, p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch,      \
+                     p->n_groups, p->seqlen, p->dstate, out)
+  if (np == 8) MC_BCQ(8);
+  else if (np == 16) MC_BCQ(16);
+  else MC_BCQ(32);
+#undef MC_BCQ
+  return hipGetLastError();
+}
+
+// dB / dC: sum the per-workgroup slabs; dA / dD / dbias: sum the per-batch slabs.
 template <typename TW, int kN>
 __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, int G, int nblk,
                                                            int dstate, int L, TW* __restrict__ dB, TW* __restrict__ dC) {
@@ -639,9 +646,9 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
 
 // Column sums over the batch: out[c] = sum_b in[b][c] (row stride ld).  A
 // block = 32 columns x 8 batch lanes; the 8 partials meet in LDS in a fixed
-// order (deterministic).  Used for dA (cols = (d, n)), dD and dbias (cols = d).
+// order (deterministic).  Used for dD and dbias (cols = d).
 __global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__ in, int batch, int cols, int64_t ld,
-                                                       int out_cols, int col_div, int col_mod, float* __restrict__ out) {
+                                                       float* __restrict__ out) {
   __shared__ float part[8][33];
   const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cx;
@@ -654,11 +661,8 @@ __global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += part[k][cx];
-    // column c of the slab -> output index (drop padded states: c = d*col_div + n, keep n < col_mod)
-    const int d = c / col_div, n = c % col_div;
-    if (n < col_mod) out[(int64_t)d * col_mod + n] = t;
+    out[c] = t;
   }
-  (void)out_cols;
 }
 
 // dA[d][n] = sum_b slab[b][n][d] (slab row stride ld): columns c = n * dim + d
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(256) void scan_bwd_colsum_nd(const float* __restric
 }
 
 struct BwdWs {
-  size_t bct, slab_bc, slab_a, slab_d, slab_bias, total;
+  size_t bq, slab_bc, slab_a, slab_d, slab_bias, total;
 };
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
@@ -692,7 +696,7 @@ static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
   const int nblk = (dim / G + kRows - 1) / kRows;
   BwdWs w;
   size_t o = 0;
-  w.bct = o; o += align256(bct_bytes(batch, seqlen, dstate, G));
+  w.bq = o; o += align256((size_t)batch * G * seqlen * (np / 2) * 16);
   w.slab_bc = o; o += align256((size_t)batch * G * nblk * np * 2 * seqlen * 4);
   w.slab_a = o; o += align256((size_t)batch * dim * np * 4);
   w.slab_d = o; o += align256((size_t)batch * dim * 4);
@@ -702,19 +706,26 @@ static BwdWs bwd_ws_layout(int batch, int dim, int seqlen, int dstate, int G) {
 }
 
 template <typename TI, int kN>
+static size_t bwd_lds_bytes() {
+  constexpr int kP = kN / 2, kPW = kP / 2;
+  return 4 * (size_t)ChunkRows<TI>::kBytes + (size_t)2 * (kSub - 1) * kPW * kRows * 8 + (size_t)kTC * kP * 16 +
+         (size_t)2 * kRows * 3 * (kTB / 2) * 4 + (size_t)kTB * 2 * kN * 4;
+}
+
+template <typename TI, int kN>
 static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
-  // B/C quads + carry, dA, x0, A + the tile's dB / dC sums
-  const size_t lds = (size_t)(kN / 2) * kTB * 16 + (size_t)4 * (kN / 2) * kRows * 8 + (size_t)kTB * 2 * kN * 4;
-  // 16-bit rows in groups of 2 tiles.  Groups of 4 (one wave per SIMD for the
-  // registers) measured slower: C2 780 vs 724 us contiguous, 810 vs 817 us
-  // with the mixer's channel-major views (tools/ab_scan_bwd.sh)
-  if (aligned && sizeof(TI) == 2) {
-    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, 2>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  } else if (aligned) {
-    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, 1>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  } else {
-    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, 1>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  }
+  const size_t lds = bwd_lds_bytes<TI, kN>();
+  // 2 waves per SIMD where registers and LDS allow it (16-bit rows, kN <= 16): <= 256 VGPRs,
+  // <= 40 KB LDS per workgroup; fp32 rows or kN = 32 run at one wave per SIMD.
+  constexpr int kMinW = (sizeof(TI) == 2 && kN <= 16) ? 2 : 1;
+  if (aligned && a.softplus)
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, true, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+  else if (aligned)
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, false, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+  else if (a.softplus)
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, true, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+  else
+    hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, false, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
@@ -740,10 +751,10 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
                      (int64_t)a.dim * kN, dA);
   if (dD)
     hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_d, a.batch, a.dim,
-                       (int64_t)a.dim, a.dim, 1, 1, dD);
+                       (int64_t)a.dim, dD);
   if (dbias)
     hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_bias, a.batch, a.dim,
-                       (int64_t)a.dim, a.dim, 1, 1, dbias);
+                       (int64_t)a.dim, dbias);
 }
 
 template <typename TW>
@@ -784,20 +795,23 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   }
   MC_CHECK(p->u && p->delta && p->B && p->C && p->dout && p->du && p->ddelta && p->dB && p->dC, MC_ERR_INVALID,
            "mc_scan_bwd: u, delta, B, C, dout and du, ddelta, dB, dC must be non-null");
-  MC_CHECK(!p->z || (p->dz && p->out_y), MC_ERR_INVALID,
-           "mc_scan_bwd: dz and out_y (the forward's pre-gate output) required when z is given");
-  MC_CHECK((int64_t)kRows * mc_scan_n_chunks(p->seqlen) * padded_dstate(p->dstate) * 4 < ((int64_t)1 << 31),
-           MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit chunk-state offsets", p->seqlen);
+  MC_CHECK(!p->z || p->dz, MC_ERR_INVALID, "mc_scan_bwd: dz required when z is given");
+  MC_CHECK((int64_t)kRows * mc_scan_n_chunks(p->seqlen) * p->dstate * 4 < ((int64_t)1 << 31) &&
+               (int64_t)p->seqlen * (np / 2) * 16 < ((int64_t)1 << 31) &&
+               (int64_t)p->seqlen * 2 * np * 4 < ((int64_t)1 << 31),
+           MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit offsets", p->seqlen);
   MC_CHECK(p->chunk_states, MC_ERR_INVALID, "mc_scan_bwd: chunk_states (from the training forward) required");
   const BwdWs w = bwd_ws_layout(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups);
   MC_CHECK(p->workspace && p->workspace_bytes >= w.total && (reinterpret_cast<uintptr_t>(p->workspace) & 255) == 0,
            MC_ERR_WORKSPACE, "mc_scan_bwd: workspace must be >= %zu bytes and 256-B aligned (got %zu)", w.total,
            p->workspace_bytes);
   char* ws = reinterpret_cast<char*>(p->workspace);
-  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
-                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
-                             p->seqlen, p->dstate, reinterpret_cast<float*>(ws + w.bct), s);
-  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: B/C relayout launch failed: %s", hipGetErrorString(e));
+  hipError_t e;
+  f32x4* bq = reinterpret_cast<f32x4*>(ws + w.bq);
+  if (p->wtype == MC_DTYPE_F32) e = launch_bc_quads<float>(p, np, bq, s);
+  else if (p->wtype == MC_DTYPE_BF16) e = launch_bc_quads<bf16_t>(p, np, bq, s);
+  else e = launch_bc_quads<f16_t>(p, np, bq, s);
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: B/C quad relayout launch failed: %s", hipGetErrorString(e));
 
   BwdArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
@@ -811,37 +825,33 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   a.z_bs = p->z_batch_stride; a.z_ds = p->z_dim_stride;
   a.go_bs = p->dout_batch_stride; a.go_ds = p->dout_dim_stride;
   a.u = p->u; a.delta = p->delta; a.z = p->z; a.dout = p->dout;
-  a.A = p->A; a.bct = reinterpret_cast<const float*>(ws + w.bct); a.D = p->D; a.delta_bias = p->delta_bias;
+  a.A = p->A; a.bq = reinterpret_cast<const float*>(bq); a.D = p->D; a.delta_bias = p->delta_bias;
   a.chunk_states = p->chunk_states;
   a.du = p->du; a.ddelta = p->ddelta; a.dz = p->dz;
   a.du_bs = p->du_batch_stride; a.du_ds = p->du_dim_stride;
   a.ddt_bs = p->ddelta_batch_stride; a.ddt_ds = p->ddelta_dim_stride;
   a.dz_bs = p->dz_batch_stride; a.dz_ds = p->dz_dim_stride;
-  a.y = p->z ? p->out_y : nullptr; a.y_bs = p->out_y_batch_stride; a.y_ds = p->out_y_dim_stride;
   a.slab_bc = reinterpret_cast<float*>(ws + w.slab_bc);
   a.slab_a = reinterpret_cast<float*>(ws + w.slab_a);
   a.slab_d = reinterpret_cast<float*>(ws + w.slab_d);
   a.slab_bias = reinterpret_cast<float*>(ws + w.slab_bias);
-  (void)np;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
-  // outputs are contiguous: the vector path also needs 16-B aligned rows there
   bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
-                       vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
-                       vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
-                       vec_ok(p->dout, p->dout_batch_stride, p->dout_dim_stride, 0, ib) &&
-                       vec_ok(p->du, p->du_batch_stride, p->du_dim_stride, 0, ib) &&
-                       vec_ok(p->ddelta, p->ddelta_batch_stride, p->ddelta_dim_stride, 0, ib) &&
-                       vec_ok(p->dz, p->dz_batch_stride, p->dz_dim_stride, 0, ib) &&
-                       vec_ok(a.y, a.y_bs, a.y_ds, 0, ib);
-  // the vector path addresses a wave's 64 rows with 32-bit byte offsets
-  auto span_ok = [&](const void* t, int64_t ds) {
-    return !t || ((int64_t)(kRows - 1) * (ds < 0 ? -ds : ds) + p->seqlen) * ib < ((int64_t)1 << 31);
+                 vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
+                 vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
+                 vec_ok(p->dout, p->dout_batch_stride, p->dout_dim_stride, 0, ib) &&
+                 vec_ok(p->du, p->du_batch_stride, p->du_dim_stride, 0, ib) &&
+                 vec_ok(p->ddelta, p->ddelta_batch_stride, p->ddelta_dim_stride, 0, ib) &&
+                 vec_ok(p->dz, p->dz_batch_stride, p->dz_dim_stride, 0, ib);
+  // the vector path addresses a workgroup's 64 rows with 32-bit byte offsets
+  auto span_ok = [&](const void* t, int64_t ds) __attribute__((always_inline)) {
+    return !t || ((int64_t)(kRows - 1) * (ds < 0 ? -ds : ds) + p->seqlen + kTC) * ib < ((int64_t)1 << 31);
   };
   const bool spans = span_ok(p->u, p->u_dim_stride) && span_ok(p->delta, p->delta_dim_stride) &&
                      span_ok(p->z, p->z_dim_stride) && span_ok(p->dout, p->dout_dim_stride) &&
                      span_ok(p->du, p->du_dim_stride) && span_ok(p->ddelta, p->ddelta_dim_stride) &&
-                     span_ok(p->dz, p->dz_dim_stride) && span_ok(a.y, a.y_ds);
+                     span_ok(p->dz, p->dz_dim_stride);
   aligned = aligned && spans;
   if (p->itype == MC_DTYPE_F32) rc = launch_bwd_t<float>(a, aligned, s);
   else if (p->itype == MC_DTYPE_BF16) rc = launch_bwd_t<bf16_t>(a, aligned, s);

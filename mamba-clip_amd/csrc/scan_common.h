@@ -8,7 +8,7 @@ namespace mc {
 namespace scan {
 
 constexpr int kT = 32;             // sequence positions per forward tile
-constexpr int kS = MC_SCAN_CHUNK;  // positions per saved chunk state (8)
+constexpr int kS = MC_SCAN_CHUNK;  // positions per saved chunk state (32)
 constexpr int kRows = 64;          // channels per workgroup: one wave
 
 // B/C as the recurrence consumes them: fp32, position-major, [b][g][l][2*kNp]

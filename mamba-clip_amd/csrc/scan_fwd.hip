@@ -327,7 +327,7 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
   constexpr int kQ = kN / 4;
   constexpr int kW = kRows * kR;                  // channels per wave
   constexpr int kVL = kR * kVPR;                  // staged vectors per lane per array
-  static_assert(kTP % kS == 0, "chunk-state positions must be static within a chunk");
+  static_assert(kS % kTP == 0, "saved states fall on chunk ends");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* rowbuf = smem;                            // [kW][RL::kStride]
@@ -460,30 +460,35 @@ __global__ __launch_bounds__(kRows, kR == 1 ? 3 : 1) void scan_fwd_mc_kernel(con
         }
         const f32x2 ys = ya + yb;
         reinterpret_cast<float*>(rowbuf + (lane + kRows * r) * RL::kStride)[tt] = fmaf(Dv[r], uv, ys.x + ys.y);
-        const int row = lane + kRows * r;
-        if (((tt + 1) % kS) == 0 && a.chunk_states && row < nrows) {
-          const int sc = (t + 1) / kS - 1;
-          if (sc < a.n_states) {
-            float* cs = a.chunk_states + (((int64_t)b * a.dim + dbase + row) * a.n_states + sc) * a.dstate;
-            if ((a.dstate & 3) == 0) {
-#pragma unroll
-              for (int n4 = 0; n4 < kN / 4; ++n4)
-                if (n4 * 4 < a.dstate)
-                  reinterpret_cast<float4*>(cs)[n4] =
-                      make_float4(x[r][2 * n4].x, x[r][2 * n4].y, x[r][2 * n4 + 1].x, x[r][2 * n4 + 1].y);
-            } else {
-#pragma unroll
-              for (int n = 0; n < kN; ++n)
-                if (n < a.dstate) cs[n] = (n & 1) ? x[r][n / 2].y : x[r][n / 2].x;
-            }
-          }
-        }
       }
     };
 #pragma unroll
     for (int tt = 0; tt < kTP; tt += 2) {
       step(tt, bcA, bcB);
       step(tt + 1, bcB, bcA);
+    }
+    // saved state after every kS positions and after the last chunk (positions
+    // past L froze the state, so that one is the state after position L-1)
+    if (a.chunk_states && (((l0 + kTP) % kS) == 0 || ch == n_chunks - 1)) {
+      const int sc = (l0 + kTP + kS - 1) / kS - 1;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int row = lane + kRows * r;
+        if (row < nrows && sc < a.n_states) {
+          float* cs = a.chunk_states + (((int64_t)b * a.dim + dbase + row) * a.n_states + sc) * a.dstate;
+          if ((a.dstate & 3) == 0) {
+#pragma unroll
+            for (int n4 = 0; n4 < kN / 4; ++n4)
+              if (n4 * 4 < a.dstate)
+                reinterpret_cast<float4*>(cs)[n4] =
+                    make_float4(x[r][2 * n4].x, x[r][2 * n4].y, x[r][2 * n4 + 1].x, x[r][2 * n4 + 1].y);
+          } else {
+#pragma unroll
+            for (int n = 0; n < kN; ++n)
+              if (n < a.dstate) cs[n] = (n & 1) ? x[r][n / 2].y : x[r][n / 2].x;
+          }
+        }
+      }
     }
     wave_lds_sync();
 

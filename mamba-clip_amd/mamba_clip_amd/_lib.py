@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB", os.path.join(_HERE, "libmamba_clip_amd.so"))
 
 MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3 = 0, 1, 2, 3
-MC_SCAN_CHUNK = 8
+MC_SCAN_CHUNK = 32
 MC_SCAN_MAX_DSTATE = 32
 
 c_i32, c_i64, c_vp, c_fp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p

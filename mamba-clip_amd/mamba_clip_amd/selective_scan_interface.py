@@ -59,9 +59,9 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
 def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False):
     """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None[, out_y]).
 
-    ``want_y`` (training with z): also return the pre-gate output y + D u that
-    the backward's dz needs -- upstream's forward returns it as ``out`` next to
-    ``out_z``.
+    ``want_y`` (with z): also return the pre-gate output y + D u -- upstream's
+    forward returns it as ``out`` next to ``out_z``.  Training does not need it:
+    the backward recomputes y from the chunk states.
     """
     lib = _lib.load()
     batch, dim, L = u.shape
@@ -101,7 +101,7 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, out_y=None):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
     lib = _lib.load()
     batch, dim, L = u.shape
     dstate = A.shape[1]
@@ -138,8 +138,6 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
     p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
     p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
-    if out_y is not None:
-        p.out_y, p.out_y_batch_stride, p.out_y_dim_stride = out_y.data_ptr(), out_y.stride(0), out_y.stride(1)
     _lib.check(lib.mc_scan_bwd(p, _lib.stream_handle(u.device)), "mc_scan_bwd")
     return du, ddelta, dA, dB, dC, dD, dz, dbias
 
@@ -158,12 +156,10 @@ class SelectiveScanFn(torch.autograd.Function):
         bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
         _check_inputs(u, delta, A32, B, C, D32, z, bias32)
         need_grad = any(ctx.needs_input_grad[:8])
-        res = scan_fwd(u, delta, A32, B, C, D32, z, bias32, delta_softplus,
-                       want_states=need_grad, want_last=return_last_state, want_y=need_grad)
-        out, states, last = res[:3]
-        out_y = res[3] if need_grad else None
+        out, states, last = scan_fwd(u, delta, A32, B, C, D32, z, bias32, delta_softplus,
+                                     want_states=need_grad, want_last=return_last_state)
         if need_grad:
-            ctx.save_for_backward(u, delta, A32, B, C, D32, z, bias32, states, out_y)
+            ctx.save_for_backward(u, delta, A32, B, C, D32, z, bias32, states)
         ctx.delta_softplus = delta_softplus
         ctx.squeeze = (squeeze_B, squeeze_C)
         ctx.dtypes = (A.dtype, D.dtype if D is not None else None,
@@ -173,9 +169,9 @@ class SelectiveScanFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, *args):
-        u, delta, A32, B, C, D32, z, bias32, states, out_y = ctx.saved_tensors
+        u, delta, A32, B, C, D32, z, bias32, states = ctx.saved_tensors
         du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, delta, A32, B, C, D32, z, bias32,
-                                                         ctx.delta_softplus, dout, states, out_y)
+                                                         ctx.delta_softplus, dout, states)
         if ctx.squeeze[0]:
             dB = dB.squeeze(1)
         if ctx.squeeze[1]:
