@@ -50,7 +50,10 @@ struct FwdArgs {
 // At C4 (B=64, D=3072: 3072 one-wave workgroups on 1024 SIMDs) the kernel is
 // VALU + v_exp issue bound (~33 SIMD cycles per wave per (t, n) step, measured
 // the same at 1 and 2 waves per SIMD), not HBM bound.
-template <typename TI, int kN, bool kAligned, int kG, bool kPBC, bool kPU, int kMinW>
+// kAligned: 0 = element-wise rows, 1 = 16-B aligned rows, 2 = aligned and every chunk
+// full (seqlen % kT == 0: no masked-load code at all, which keeps the register
+// budget of the 3-waves-per-SIMD build free of spills)
+template <typename TI, int kN, int kAligned, int kG, bool kPBC, bool kPU, int kMinW>
 __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a) {
   using RL = RowLayout<TI>;
   constexpr int VI = RL::VI;                    // elements per 16-B vector
@@ -76,19 +79,37 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   const TI* __restrict__ dl = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs;
   const TI* __restrict__ zp = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs;
   TI* __restrict__ out = reinterpret_cast<TI*>(a.out) + (int64_t)b * a.o_bs;
+  // (whole-chunk mode) this wave's rows of u / delta / z / out as buffer ranges: 32-bit offsets
+  auto rows_rsrc = [&](const void* base, int64_t ds) {
+    return make_rsrc(reinterpret_cast<const TI*>(base) + (int64_t)dbase * ds,
+                     (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)));
+  };
+  const __amdgpu_buffer_rsrc_t rs_out = rows_rsrc(out, a.o_ds);
+  const __amdgpu_buffer_rsrc_t rs_u = rows_rsrc(u, a.u_ds), rs_d = rows_rsrc(dl, a.dt_ds);
+  const __amdgpu_buffer_rsrc_t rs_z = rows_rsrc(hasZ ? (const void*)zp : (const void*)u, hasZ ? a.z_ds : a.u_ds);
+  const __amdgpu_buffer_rsrc_t rs_y =
+      rows_rsrc(a.out_y ? (const void*)(reinterpret_cast<const TI*>(a.out_y) + (int64_t)b * a.y_bs) : (const void*)u,
+                a.out_y ? a.y_ds : a.u_ds);
 
   // ---- per-channel constants
   const int my_d = dbase + lane;
   const bool my_ok = lane < nrows;
   // states are processed in pairs with packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32)
+  // unconditional loads (clamped row / state index), masked afterwards: no load behind a branch
   f32x2 A2[kN / 2];
+  const int my_dc = dbase + min(lane, nrows - 1);
+  {
+    float av[kN];
 #pragma unroll
-  for (int n = 0; n < kN; ++n) {
-    const float v = (my_ok && n < a.dstate) ? a.A[(int64_t)my_d * a.dstate + n] * kLog2e : 0.f;
-    if (n & 1) A2[n / 2].y = v; else A2[n / 2].x = v;
+    for (int n = 0; n < kN; ++n) av[n] = a.A[(int64_t)my_dc * a.dstate + min(n, a.dstate - 1)];
+#pragma unroll
+    for (int n = 0; n < kN; ++n) {
+      const float v = (my_ok && n < a.dstate) ? av[n] * kLog2e : 0.f;
+      if (n & 1) A2[n / 2].y = v; else A2[n / 2].x = v;
+    }
   }
-  const float Dv = (my_ok && a.D) ? a.D[my_d] : 0.f;
-  const float biasv = (my_ok && a.delta_bias) ? a.delta_bias[my_d] : 0.f;
+  const float Dv = (my_ok && a.D) ? a.D[my_dc] : 0.f;
+  const float biasv = (my_ok && a.delta_bias) ? a.delta_bias[my_dc] : 0.f;
 
   f32x2 x[kN / 2];
 #pragma unroll
@@ -100,7 +121,20 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   constexpr int kBCPer = (kBCVec + kRows - 1) / kRows;
   uint4 pu[kVPR], pd[kVPR];
   float4 pbc[kPBC ? kBCPer : 1];
+  // (whole-chunk mode) this (batch, group)'s B/C rows as a buffer range: chunks past
+  // the end read 0, so the prefetch needs no branch (a branch around loads makes the
+  // compiler drain the stores issued after them before the loads may be consumed)
+  const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(a.bct + (int64_t)bg * L_ * (2 * kN), (uint32_t)L_ * (2 * kN) * 4u);
   auto load_bc = [&](int l0, float4 (&dst)[kBCPer]) {
+    if constexpr (kAligned == 2) {
+#pragma unroll
+      for (int k = 0; k < kBCPer; ++k) {
+        const int v = lane + k * kRows;
+        const uint32_t off = v < kBCVec ? (uint32_t)(l0 * (2 * kN) + 4 * v) * 4u : 0x80000000u;
+        dst[k] = __builtin_bit_cast(float4, buf_ld16(rs_bc, off));
+      }
+      return;
+    }
     const float4* src = reinterpret_cast<const float4*>(a.bct + ((int64_t)bg * L_ + l0) * (2 * kN));
     const int nvec = min(kT, L_ - l0) * (2 * kN) / 4;
 #pragma unroll
@@ -110,13 +144,18 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
     }
   };
   auto load_regs = [&](int l0) {
-    const bool full = kAligned && (l0 + kT <= L_);
+    const bool full = kAligned == 2 || (kAligned == 1 && l0 + kT <= L_);
 #pragma unroll
     for (int k = 0; k < kVPR; ++k) {
       const int j = lane + k * kRows;
       const int r = j / kVPR, c = j % kVPR;
       const int rr = min(r, nrows - 1);   // rows past the group end: load a valid row, never stored
       const int col0 = l0 + c * VI;
+      if constexpr (kAligned == 2) {   // 32-bit offsets into the wave's row block (no 64-bit pointers)
+        pu[k] = buf_ld16(rs_u, (uint32_t)(rr * a.u_ds + col0) * (uint32_t)sizeof(TI));
+        pd[k] = buf_ld16(rs_d, (uint32_t)(rr * a.dt_ds + col0) * (uint32_t)sizeof(TI));
+        continue;
+      }
       const TI* su = u + (int64_t)(dbase + rr) * a.u_ds + col0;
       const TI* sd = dl + (int64_t)(dbase + rr) * a.dt_ds + col0;
       if (full) {
@@ -134,7 +173,7 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   if constexpr (kPU) load_regs(0);
   for (int ch = 0; ch < a.n_chunks; ++ch) {
     const int l0 = ch * kT;
-    const bool full = kAligned && (l0 + kT <= L_);
+    const bool full = kAligned == 2 || (kAligned == 1 && l0 + kT <= L_);
     if constexpr (!kPU) load_regs(l0);   // other resident waves cover the latency
 
     // ---- stage u / delta (vector j = lane + k*64 -> row j / kVPR, col j % kVPR) and B/C
@@ -162,7 +201,26 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
     }
     wave_lds_sync();
     if constexpr (kPU) {
-      if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
+      if constexpr (kAligned == 2) load_regs(l0 + kT);   // past the end: out-of-range offsets read 0
+      else if (ch + 1 < a.n_chunks) load_regs(l0 + kT);
+    }
+    // this chunk's z vectors (gate pass mapping), loaded now so that they arrive
+    // under the recurrence instead of stalling the gate pass
+    uint4 cz[kVPR];
+    if (hasZ) {
+      const int ln = kAligned == 2 ? opaque_lane_id() : lane;   // rebuilt here, not held live
+#pragma unroll
+      for (int k = 0; k < kVPR; ++k) {
+        const int j = ln + k * kRows;
+        const int r = j / kVPR, c = j % kVPR;
+        const int col0 = l0 + c * VI;
+        if constexpr (kAligned == 2) {
+          cz[k] = buf_ld16(rs_z, (uint32_t)(min(r, nrows - 1) * a.z_ds + col0) * (uint32_t)sizeof(TI));
+        } else {
+          const TI* zs = zp + (int64_t)(dbase + min(r, nrows - 1)) * a.z_ds + col0;
+          cz[k] = full ? ld16(zs) : ld16_masked(zs, max(0, min(VI, L_ - col0)));
+        }
+      }
     }
 
     // ---- the recurrence over this chunk, one channel per lane.  Steps go
@@ -250,9 +308,10 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
     wave_lds_sync();
 
     // ---- gate + store, coalesced along the sequence (same vector mapping)
+    const int lg = kAligned == 2 ? opaque_lane_id() : lane;   // offsets rebuilt, not held live
 #pragma unroll
     for (int k = 0; k < kVPR; ++k) {
-      const int j = lane + k * kRows;
+      const int j = lg + k * kRows;
       const int r = j / kVPR, c = j % kVPR;
       const int col0 = l0 + c * VI;
       const int nv = max(0, min(VI, L_ - col0));
@@ -269,17 +328,25 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
       }
       if (hasZ) {
         if (a.out_y && r < nrows) {
-          TI* ydst = reinterpret_cast<TI*>(a.out_y) + (int64_t)b * a.y_bs + (int64_t)(dbase + r) * a.y_ds + col0;
-          const uint4 yq = pack_f<TI>(o);
-          if (full) st16(ydst, yq);
-          else st16_masked(ydst, yq, nv);
+          if constexpr (kAligned == 2) {
+            buf_st16(rs_y, (uint32_t)(r * a.y_ds + col0) * (uint32_t)sizeof(TI), pack_f<TI>(o));
+          } else {
+            TI* ydst = reinterpret_cast<TI*>(a.out_y) + (int64_t)b * a.y_bs + (int64_t)(dbase + r) * a.y_ds + col0;
+            const uint4 yq = pack_f<TI>(o);
+            if (full) st16(ydst, yq);
+            else st16_masked(ydst, yq, nv);
+          }
         }
-        const TI* zs = zp + (int64_t)(dbase + min(r, nrows - 1)) * a.z_ds + col0;
-        const uint4 zq = full ? ld16(zs) : ld16_masked(zs, nv);
 #pragma unroll
-        for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(zq, e));
+        for (int e = 0; e < VI; ++e) o[e] *= silu_f(elem_f<TI>(cz[k], e));
       }
-      if (r < nrows) {
+      if constexpr (kAligned == 2) {
+        // whole chunks: every lane stores (rows past the group end fall outside the
+        // buffer range and are dropped), so the store count is static and the next
+        // chunk's prefetch wait does not have to drain these stores
+        const uint32_t off = r < nrows ? (uint32_t)(r * a.o_ds + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
+        buf_st16(rs_out, off, pack_f<TI>(o));
+      } else if (r < nrows) {
         TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
         const uint4 ov = pack_f<TI>(o);
         if (full) st16(dst, ov);
@@ -562,10 +629,17 @@ static int launch_fwd_mc(const FwdArgs& a0, bool aligned, hipStream_t s) {
 template <typename TI, int kN, int kG, bool kPBC, bool kPU, int kMinW>
 static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
   const size_t lds = (size_t)kRows * RowLayout<TI>::kStride + (size_t)kT * 2 * kN * 4;
-  if (aligned)
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, true, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  auto fits = [&](int64_t ds) {
+    return ((int64_t)(kRows - 1) * (ds < 0 ? -ds : ds) + a.seqlen) * (int64_t)sizeof(TI) < ((int64_t)1 << 31);
+  };
+  const bool span32 = fits(a.o_ds) && fits(a.u_ds) && fits(a.dt_ds) && (!a.z || fits(a.z_ds)) &&
+                      (!a.out_y || fits(a.y_ds));
+  if (aligned && a.seqlen % kT == 0 && span32)
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 2, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
+  else if (aligned)
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 1, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
   else
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, false, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s,
+    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 0, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s,
                        a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
@@ -582,7 +656,8 @@ static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
 // vector-load B/C rings spill at the occupancy they need.  With short
 // sequences the grid is many short-lived waves and the SGPR-fed kernel wins;
 // with long ones the LDS-staged kernel's deeper prefetch wins.
-// MC_SCAN_FWD_VARIANT overrides the choice for A/B runs: 0 = LDS-staged, 10 = SGPR R=1, 8 = SGPR R=3.
+// MC_SCAN_FWD_VARIANT overrides the choice for A/B runs: 0 = LDS-staged (3 w/SIMD), 2 = LDS-staged
+// (2 w/SIMD), 10 = SGPR R=1, 8 = SGPR R=3.
 static int fwd_variant() {
   static const int v = [] {
     const char* e = getenv("MC_SCAN_FWD_VARIANT");
@@ -598,6 +673,11 @@ static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
   switch (v) {
     case 8: return launch_fwd_mc<TI, kN, 3>(a, aligned, s);
     case 10: return launch_fwd_mc<TI, kN, 1>(a, aligned, s);
+    case 2: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
+    case 3: if (aligned && a.seqlen % kT == 0) return launch_fwd_v<TI, kN, 4, true, true, 3>(a, aligned, s);
+            return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
+    case 4: if (aligned && a.seqlen % kT == 0) return launch_fwd_v<TI, kN, 2, false, true, 3>(a, aligned, s);
+            return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
     default: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
   }
 }
