@@ -87,6 +87,55 @@ int mc_ce_grad(int32_t rows, int32_t cols, const float* S, int64_t lds, const fl
                size_t workspace_bytes, void* stream);
 size_t mc_ce_grad_workspace_bytes(int32_t rows, int32_t cols);
 
+/* Fused logits + softmax cross-entropy (no M x N matrix in memory).
+ *   S[i, j] = scale * sx[i] * sy[j] * sum_k X[i, k] Y[j, k]        (never stored)
+ *   loss    = coef_r * sum_i (lse_r[i] - S[i, i + row_off])
+ *           + coef_c * sum_j (lse_c[j] - S[j + col_off, j])        (column term iff lse_c != NULL)
+ * mc_ce_fused_fwd: the GEMM tiles of mc_gemm_nt reduce their logits in
+ * registers to per-row / per-column (max, sum exp) partials and target logits;
+ * a second kernel folds them into lse_r (M), lse_c (N) and *loss_out.  The
+ * workspace holds the partials (mc_ce_fused_fwd_workspace_bytes; about
+ * 8 * (M * ceil(N/128) + N * ceil(M/128)) bytes).
+ * mc_ce_fused_grad: recomputes the same tiles from (lse_r, lse_c) and writes
+ *   G[i, j] = gmul * gout * ( coef_r (exp(S_ij - lse_r[i]) - [j == i + row_off])
+ *                           + coef_c (exp(S_ij - lse_c[j]) - [i == j + col_off]) )
+ * with gmul = scale if g_times_scale else 1 (so G @ Y is dX directly) and,
+ * if dscale_out != NULL, *dscale_out = sum_ij G_ij S_ij / (gmul * scale):
+ * the logit_scale gradient.  lse_r or lse_c NULL drops that term.  Called on
+ * a block of rows of X (or, with the roles swapped, of Y) it yields one
+ * block of dS (or dS^T) at a time, so the backward never holds M x N either.
+ * Row / column offsets must satisfy |off| < 2^30.  in_dtype: bf16, fp32 or
+ * fp8 e4m3 (fp8: forward only is meaningful, operands from mc_quant_rows_fp8
+ * with sx / sy their inverse scales).
+ * Replaces ClipLoss.get_logits + the two F.cross_entropy calls
+ * (loss.py:89-147) and their autograd backward. */
+typedef struct mc_ce_fused_params {
+  int32_t M, N, K;
+  int32_t in_dtype;
+  const void* X; int64_t ldx;
+  const void* Y; int64_t ldy;
+  const float* row_scale_x;     /* sx, nullable */
+  const float* row_scale_y;     /* sy, nullable */
+  float scale;                  /* used when scale_dev == NULL */
+  const float* scale_dev;
+  int64_t row_off; float coef_r;
+  int64_t col_off; float coef_c;
+  float* lse_r;                 /* fwd: out (M);  grad: in, nullable */
+  float* lse_c;                 /* fwd: out (N), NULL = no column term;  grad: in, nullable */
+  float* loss_out;              /* fwd: device scalar */
+  const float* gout_dev;        /* grad: upstream scalar, NULL = 1 */
+  int32_t g_dtype;              /* grad: fp32 or bf16 */
+  int32_t g_times_scale;
+  void* G; int64_t ldg;         /* grad: M x N block */
+  float* dscale_out;            /* grad: device scalar, nullable */
+  void* workspace; size_t workspace_bytes;
+} mc_ce_fused_params;
+
+int mc_ce_fused_fwd(const mc_ce_fused_params* p, void* stream);
+size_t mc_ce_fused_fwd_workspace_bytes(int32_t M, int32_t N, int32_t with_columns);
+int mc_ce_fused_grad(const mc_ce_fused_params* p, void* stream);
+size_t mc_ce_fused_grad_workspace_bytes(int32_t M, int32_t N);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,16 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int c_vec;                           // C 16-B aligned and ldc % 4 == 0: vector stores in full tiles
   int c_vec16;                         // 16-bit C: ldc % 8 == 0 as well (16-B stores of 8 values)
+  // fused cross-entropy epilogues (kEpi 1 = statistics, 2 = gradient).  Labels:
+  // row i's target column is i + off_r, column j's target row is j + off_c.
+  int off_r, off_c;
+  float coef_r, coef_c;
+  const float* lse_r; const float* lse_c;   // kEpi 2 inputs; NULL drops that term
+  const float* gout_dev;                    // kEpi 2 upstream scalar (NULL = 1)
+  int g_times_alpha;                        // kEpi 2: store alpha * G (then G @ Y is dX directly)
+  float2* rpart; float2* cpart;             // kEpi 1: (max, sumexp) partials [tiles_n][M], [tiles_m][N]
+  float* tgt_r; float* tgt_c;               // kEpi 1: target logits (written by the tile holding them)
+  float* gpart;                             // kEpi 2: per-workgroup sum(G * S), nullable
 };
 
 typedef uint8_t fp8_t;   // OCP e4m3fn bits
@@ -56,7 +66,156 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <typename TIn, typename TOut, bool kAligned>
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mm = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+  m = mm;
+}
+
+// Statistics epilogue of the fused logits + cross-entropy forward: the 128x128
+// logit tile never leaves registers.  Each wave reduces its 64x64 quadrant to
+// per-row and per-column (max, sum exp) partials with a transpose-reduce
+// (every shuffle step halves the entries a lane carries, so 16 row entries
+// need 15 exchanges, not 64), the two waves sharing rows / columns merge
+// through LDS, and one (max, sumexp) per row and tile column-block lands in
+// rpart[tn][row] (cpart[tm][col] likewise).  The tiles that hold a label
+// also record the target logit.  ce_fused_reduce_kernel folds the partials.
+__device__ __forceinline__ void ce_stats_epilogue(const GemmArgs& g, f32x4 (&acc)[4][4], const float (&row_scale)[4][4],
+                                                  const float (&col_scale)[4], float alpha, int row_base, int col_base,
+                                                  char* lds, int tm, int tn, int m0, int n0) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = (row_base + i * 16 + r < g.M) && (col_base + j * 16 < g.N);
+        acc[i][j][r] = ok ? (acc[i][j][r] * row_scale[i][r]) * (alpha * col_scale[j]) : -INFINITY;
+      }
+  const int dbase = col_base - row_base;   // col - row of acc[0][0][0]
+  // target logits: only tiles crossing a label diagonal (uniform tests)
+  if (m0 + g.off_r < n0 + BN && m0 + BM - 1 + g.off_r >= n0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+        bool hit = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool h = dbase + 16 * (j - i) - r == g.off_r && acc[i][j][r] != -INFINITY;
+          t = h ? acc[i][j][r] : t;
+          hit = hit || h;
+        }
+        if (hit) g.tgt_r[row_base + i * 16 + r] = t;
+      }
+  }
+  const bool cols = g.cpart != nullptr;
+  if (cols && n0 + g.off_c < m0 + BM && n0 + BN - 1 + g.off_c >= m0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = 0.f;
+      bool hit = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool h = dbase + 16 * (j - i) - r == -g.off_c && acc[i][j][r] != -INFINITY;
+          t = h ? acc[i][j][r] : t;
+          hit = hit || h;
+        }
+      if (hit) g.tgt_c[col_base + j * 16] = t;
+    }
+  }
+
+  // rows: 16 entries (k = 4i + r) per lane over its 4 columns, then 4 exchange steps
+  float rm[16], rs[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int i = k >> 2, r = k & 3;
+    const float m = fmaxf(fmaxf(acc[i][0][r], acc[i][1][r]), fmaxf(acc[i][2][r], acc[i][3][r]));
+    const float mr = m == -INFINITY ? 0.f : m;
+    rm[k] = m;
+    rs[k] = (__expf(acc[i][0][r] - mr) + __expf(acc[i][1][r] - mr)) + (__expf(acc[i][2][r] - mr) + __expf(acc[i][3][r] - mr));
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int o = 8 >> st;               // partner lane distance == entries kept
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int k = 0; k < o; ++k) {
+      const float sm = hi ? rm[k] : rm[k + o], ss = hi ? rs[k] : rs[k + o];
+      float km = hi ? rm[k + o] : rm[k], ks = hi ? rs[k + o] : rs[k];
+      lse_merge(km, ks, __shfl_xor(sm, o), __shfl_xor(ss, o));
+      rm[k] = km;
+      rs[k] = ks;
+    }
+  }
+  // lane now holds row entry k = lane & 15 of its 16-lane group, over the wave's 64 columns
+  // columns: 4 entries (j) per lane over its 16 rows, then 2 exchange steps across the lane groups
+  float cm[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4 && cols; ++j) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[i][j][r]);
+    const float mr = m == -INFINITY ? 0.f : m;
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum += __expf(acc[i][j][r] - mr);
+    cm[j] = m;
+    cs[j] = sum;
+  }
+  if (cols) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int o = 2 >> st, ol = 32 >> st;
+      const bool hi = (lane & ol) != 0;
+#pragma unroll
+      for (int k = 0; k < o; ++k) {
+        const float sm = hi ? cm[k] : cm[k + o], ss = hi ? cs[k] : cs[k + o];
+        float km = hi ? cm[k + o] : cm[k], ks = hi ? cs[k + o] : cs[k];
+        lse_merge(km, ks, __shfl_xor(sm, ol), __shfl_xor(ss, ol));
+        cm[k] = km;
+        cs[k] = ks;
+      }
+    }
+  }
+  // lane holds column entry j = lane >> 4
+
+  float2* rowp = reinterpret_cast<float2*>(lds);          // [4 waves][64 rows]
+  float2* colp = rowp + 4 * 64;                            // [4 waves][64 cols]
+  __syncthreads();                                         // main-loop LDS reads done
+  {
+    const int k = lane & 15;
+    rowp[w * 64 + (k >> 2) * 16 + 4 * (lane >> 4) + (k & 3)] = make_float2(rm[0], rs[0]);
+    colp[w * 64 + (lane >> 4) * 16 + (lane & 15)] = make_float2(cm[0], cs[0]);
+  }
+  __syncthreads();
+  if (wc == 0) {            // waves 0, 2: rows of their half, both column halves
+    float2 a = rowp[w * 64 + lane];
+    const float2 b = rowp[(w + 1) * 64 + lane];
+    lse_merge(a.x, a.y, b.x, b.y);
+    const int row = m0 + wr * 64 + lane;
+    if (row < g.M) g.rpart[(int64_t)tn * g.M + row] = a;
+  }
+  if (cols && wr == 0) {    // waves 0, 1: columns of their half, both row halves
+    float2 a = colp[w * 64 + lane];
+    const float2 b = colp[(w + 2) * 64 + lane];
+    lse_merge(a.x, a.y, b.x, b.y);
+    const int col = n0 + wc * 64 + lane;
+    if (col < g.N) g.cpart[(int64_t)tm * g.N + col] = a;
+  }
+}
+
+// kEpi 0: C = alpha * sa * sb * A B^T.  kEpi 1 / 2: the same tile feeds a fused
+// softmax cross-entropy epilogue instead (statistics / gradient, see below).
+template <typename TIn, typename TOut, bool kAligned, int kEpi>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
   constexpr int E = (int)sizeof(TIn);
   constexpr int BK = kRowBytes / E;       // K elements per slice: 32 (bf16) or 16 (fp32)
@@ -131,6 +290,24 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
       row_scale[i][r] = (g.sa && row < g.M) ? g.sa[row] : 1.f;
     }
 
+  // gradient epilogue inputs, also loaded before the K loop
+  float lr[4][4], lcol[4], gout = 1.f;
+  if constexpr (kEpi == 2) {
+    gout = g.gout_dev ? *g.gout_dev : 1.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + (lane & 15);
+      lcol[j] = (g.lse_c && col < g.N) ? g.lse_c[col] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        lr[i][r] = (g.lse_r && row < g.M) ? g.lse_r[row] : 0.f;
+      }
+  }
+
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -202,6 +379,53 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
     }
   }
 
+  // Accumulator map (16x16 MFMA C/D): acc[i][j][r] is row wr*64 + i*16 + 4*(lane>>4) + r,
+  // column wc*64 + j*16 + (lane & 15) of the tile.
+  const int row_base = m0 + wr * 64 + 4 * (lane >> 4), col_base = n0 + wc * 64 + (lane & 15);
+  if constexpr (kEpi == 1) {
+    ce_stats_epilogue(g, acc, row_scale, col_scale, alpha, row_base, col_base, lds, tm, tn, m0, n0);
+    return;
+  }
+  if constexpr (kEpi == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = (acc[i][j][r] * row_scale[i][r]) * (alpha * col_scale[j]);
+  } else {
+    // G = gout * (coef_r (softmax_row - onehot) + coef_c (softmax_col - onehot)) from the
+    // recomputed logits; the labels are diagonals of col - row, so one integer compare each.
+    const bool has_r = g.lse_r != nullptr, has_c = g.lse_c != nullptr;
+    const float gmul = g.g_times_alpha ? gout * alpha : gout;
+    const int dbase = col_base - row_base;
+    float dsum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (acc[i][j][r] * row_scale[i][r]) * (alpha * col_scale[j]);
+          const int d = dbase + 16 * (j - i) - r;
+          float gv = 0.f;
+          if (has_r) gv = g.coef_r * (__expf(v - lr[i][r]) - (d == g.off_r ? 1.f : 0.f));
+          if (has_c) gv = fmaf(g.coef_c, __expf(v - lcol[j]) - (d == -g.off_c ? 1.f : 0.f), gv);
+          const bool ok = (row_base + i * 16 + r < g.M) && (col_base + j * 16 < g.N);
+          gv = ok ? gv : 0.f;
+          dsum = fmaf(gv, v, dsum);
+          acc[i][j][r] = gv * gmul;
+        }
+    if (g.gpart) {
+      __shared__ float red[4];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) dsum += __shfl_xor(dsum, o);
+      if (lane == 0) red[w] = dsum * gout;
+      __syncthreads();
+      if (tid == 0) g.gpart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+  }
+
   TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
   // Epilogue through LDS.  The 16x16 MFMA C/D map (col = lane & 15, row =
   // 4*(lane >> 4) + r) would make every store instruction write 64-B pieces of
@@ -222,11 +446,10 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col_l = j * 16 + (lane & 15);
-        const float cs = alpha * col_scale[j];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row_l = i2 * 16 + 4 * (lane >> 4) + r;
-          ep[row_l * kEpStride + col_l] = (acc[i][j][r] * row_scale[i][r]) * cs;
+          ep[row_l * kEpStride + col_l] = acc[i][j][r];
         }
       }
     }
@@ -274,11 +497,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
 }
 
 // ------------------------------------------------------------------ CE statistics
-__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
-  const float mm = fmaxf(m, m2);
-  s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
-  m = mm;
-}
 
 // one wave per row: lse and nll, per-block partial NLL sums (4 rows per block)
 __global__ __launch_bounds__(256) void ce_rows_kernel(int rows, int cols, const float* __restrict__ S, int64_t lds,
@@ -384,6 +602,44 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
   if (threadIdx.x == 0) out[0] = coef * red[0] / (divisor ? *divisor : 1.f);
 }
 
+// Folds the fused forward's tile partials: blocks [0, nbr) take rows, the rest
+// columns.  lse = m + log(s) merged over the tile partials in tile order;
+// partial[block] = coef * sum(lse - target) (fixed order: deterministic).
+__global__ __launch_bounds__(256) void ce_fused_reduce_kernel(int M, int N, int tiles_m, int tiles_n,
+                                                              const float2* __restrict__ rpart,
+                                                              const float2* __restrict__ cpart,
+                                                              const float* __restrict__ tgt_r,
+                                                              const float* __restrict__ tgt_c, int off_r, int off_c,
+                                                              float coef_r, float coef_c, float* __restrict__ lse_r,
+                                                              float* __restrict__ lse_c, int nbr,
+                                                              float* __restrict__ partial) {
+  __shared__ float red[256];
+  const bool rows = (int)blockIdx.x < nbr;
+  const int idx = (rows ? (int)blockIdx.x : (int)blockIdx.x - nbr) * 256 + threadIdx.x;
+  const int n = rows ? M : N, other = rows ? N : M, parts = rows ? tiles_n : tiles_m;
+  const float2* __restrict__ part = rows ? rpart : cpart;
+  float v = 0.f;
+  if (idx < n) {
+    float m = -INFINITY, sum = 0.f;
+    for (int k = 0; k < parts; ++k) {
+      const float2 q = part[(int64_t)k * n + idx];
+      lse_merge(m, sum, q.x, q.y);
+    }
+    const float l = m + __logf(sum);
+    const int64_t lab = (int64_t)idx + (rows ? off_r : off_c);
+    const float tgt = (lab >= 0 && lab < other) ? (rows ? tgt_r : tgt_c)[idx] : 0.f;
+    (rows ? lse_r : lse_c)[idx] = l;
+    v = (rows ? coef_r : coef_c) * (l - tgt);
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
 // G = gout * (coef_r (softmax_r - onehot_r) + coef_c (softmax_c - onehot_c)); partial sum(G * S)
 template <typename TOut>
 __global__ __launch_bounds__(256) void ce_grad_kernel(int rows, int cols, const float* __restrict__ S, int64_t lds,
@@ -455,6 +711,47 @@ constexpr int kGradGrid = 2048;
 using namespace mc;
 using namespace mc::ctr;
 
+namespace {
+template <int kEpi>
+void launch_gemm(const GemmArgs& g, int in_dtype, int out_dtype, bool aligned, hipStream_t s) {
+  const dim3 grid(g.tiles_m * g.tiles_n), block(256);
+#define MC_GEMM(TI, TO)                                                                         \
+  do {                                                                                          \
+    if (aligned) hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, true, kEpi>), grid, block, 0, s, g); \
+    else hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, false, kEpi>), grid, block, 0, s, g);       \
+  } while (0)
+  if (in_dtype == MC_DTYPE_BF16) {
+    if (out_dtype == MC_DTYPE_F32) MC_GEMM(bf16_t, float); else MC_GEMM(bf16_t, bf16_t);
+  } else if (in_dtype == MC_DTYPE_FP8_E4M3) {
+    if (out_dtype == MC_DTYPE_F32) MC_GEMM(fp8_t, float); else MC_GEMM(fp8_t, bf16_t);
+  } else {
+    if (out_dtype == MC_DTYPE_F32) MC_GEMM(float, float); else MC_GEMM(float, bf16_t);
+  }
+#undef MC_GEMM
+}
+
+// shape / alignment checks shared by the plain GEMM and the fused CE entry points
+int fill_operands(GemmArgs& g, const char* who, int M, int N, int K, int in_dtype, const void* A, int64_t lda,
+                  const void* B, int64_t ldb, bool& aligned) {
+  MC_CHECK(M > 0 && N > 0 && K >= 0, MC_ERR_SHAPE, "%s: bad shape", who);
+  MC_CHECK(in_dtype == MC_DTYPE_BF16 || in_dtype == MC_DTYPE_F32 || in_dtype == MC_DTYPE_FP8_E4M3, MC_ERR_DTYPE,
+           "%s: inputs must be bf16, fp32 or fp8 e4m3", who);
+  MC_CHECK(A && B, MC_ERR_INVALID, "%s: null operand", who);
+  g = GemmArgs{};
+  g.M = M; g.N = N; g.K = K;
+  g.A = A; g.lda = lda; g.B = B; g.ldb = ldb;
+  g.tiles_m = (M + BM - 1) / BM;
+  g.tiles_n = (N + BN - 1) / BN;
+  const int eb = in_dtype == MC_DTYPE_F32 ? 4 : (in_dtype == MC_DTYPE_FP8_E4M3 ? 1 : 2);
+  const int64_t v = 16 / eb;
+  aligned = aligned16(A) && aligned16(B) && lda % v == 0 && ldb % v == 0;
+  if (eb == 1)
+    MC_CHECK(aligned && K % 16 == 0, MC_ERR_SHAPE,
+             "%s: fp8 operands need K, lda, ldb multiples of 16 and 16-B aligned rows", who);
+  return MC_OK;
+}
+}  // namespace
+
 extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_gemm_nt: null params");
   MC_CHECK(p->M >= 0 && p->N >= 0 && p->K >= 0, MC_ERR_SHAPE, "mc_gemm_nt: negative shape");
@@ -463,37 +760,17 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   MC_CHECK(p->out_dtype == MC_DTYPE_F32 || p->out_dtype == MC_DTYPE_BF16, MC_ERR_DTYPE,
            "mc_gemm_nt: output must be fp32 or bf16");
   if (p->M == 0 || p->N == 0) return MC_OK;
-  MC_CHECK(p->A && p->B && p->C, MC_ERR_INVALID, "mc_gemm_nt: null operand");
+  MC_CHECK(p->C, MC_ERR_INVALID, "mc_gemm_nt: null C");
   GemmArgs g;
-  g.M = p->M; g.N = p->N; g.K = p->K;
-  g.A = p->A; g.lda = p->lda; g.B = p->B; g.ldb = p->ldb; g.C = p->C; g.ldc = p->ldc;
+  bool aligned;
+  const int rc = fill_operands(g, "mc_gemm_nt", p->M, p->N, p->K, p->in_dtype, p->A, p->lda, p->B, p->ldb, aligned);
+  if (rc != MC_OK) return rc;
+  g.C = p->C; g.ldc = p->ldc;
   g.alpha = p->alpha; g.alpha_dev = p->alpha_dev;
   g.sa = p->row_scale_a; g.sb = p->row_scale_b;
   g.c_vec = aligned16(p->C) && p->ldc % 4 == 0;
   g.c_vec16 = g.c_vec && p->ldc % 8 == 0;
-  g.tiles_m = (p->M + BM - 1) / BM;
-  g.tiles_n = (p->N + BN - 1) / BN;
-  const int eb = p->in_dtype == MC_DTYPE_F32 ? 4 : (p->in_dtype == MC_DTYPE_FP8_E4M3 ? 1 : 2);
-  const int64_t v = 16 / eb;
-  const bool aligned = aligned16(p->A) && aligned16(p->B) && p->lda % v == 0 && p->ldb % v == 0;
-  if (eb == 1)
-    MC_CHECK(aligned && p->K % 16 == 0, MC_ERR_SHAPE,
-             "mc_gemm_nt: fp8 operands need K, lda, ldb multiples of 16 and 16-B aligned rows");
-  hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(g.tiles_m * g.tiles_n), block(256);
-#define MC_GEMM(TI, TO)                                                                   \
-  do {                                                                                    \
-    if (aligned) hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, true>), grid, block, 0, s, g); \
-    else hipLaunchKernelGGL((gemm_nt_kernel<TI, TO, false>), grid, block, 0, s, g);       \
-  } while (0)
-  if (p->in_dtype == MC_DTYPE_BF16) {
-    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(bf16_t, float); else MC_GEMM(bf16_t, bf16_t);
-  } else if (p->in_dtype == MC_DTYPE_FP8_E4M3) {
-    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(fp8_t, float); else MC_GEMM(fp8_t, bf16_t);
-  } else {
-    if (p->out_dtype == MC_DTYPE_F32) MC_GEMM(float, float); else MC_GEMM(float, bf16_t);
-  }
-#undef MC_GEMM
+  launch_gemm<0>(g, p->in_dtype, p->out_dtype, aligned, (hipStream_t)stream);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_nt: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
@@ -590,5 +867,104 @@ extern "C" int mc_quant_rows_fp8(int32_t rows, int32_t cols, int32_t in_dtype, c
     MC_CHECK(false, MC_ERR_DTYPE, "mc_quant_rows_fp8: input must be fp32, bf16 or f16");
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_quant_rows_fp8: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+// ------------------------------------------------------------------ fused logits + CE
+namespace {
+inline size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
+
+struct FusedWs {
+  float2* rpart; float2* cpart; float* tgt_r; float* tgt_c; float* partial;
+  size_t bytes;
+};
+
+FusedWs fused_fwd_ws(int M, int N, bool cols, void* base) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int nb = (M + 255) / 256 + (cols ? (N + 255) / 256 : 0);
+  char* p = reinterpret_cast<char*>(base);
+  FusedWs w;
+  size_t off = 0;
+  w.rpart = reinterpret_cast<float2*>(p + off); off += al16((size_t)tn * M * sizeof(float2));
+  w.cpart = cols ? reinterpret_cast<float2*>(p + off) : nullptr; off += cols ? al16((size_t)tm * N * sizeof(float2)) : 0;
+  w.tgt_r = reinterpret_cast<float*>(p + off); off += al16((size_t)M * sizeof(float));
+  w.tgt_c = reinterpret_cast<float*>(p + off); off += cols ? al16((size_t)N * sizeof(float)) : 0;
+  w.partial = reinterpret_cast<float*>(p + off); off += al16((size_t)nb * sizeof(float));
+  w.bytes = off;
+  return w;
+}
+
+int fused_common(const mc_ce_fused_params* p, const char* who, GemmArgs& g, bool& aligned) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "%s: null params", who);
+  const int rc = fill_operands(g, who, p->M, p->N, p->K, p->in_dtype, p->X, p->ldx, p->Y, p->ldy, aligned);
+  if (rc != MC_OK) return rc;
+  MC_CHECK(p->row_off > -(1 << 30) && p->row_off < (1 << 30) && p->col_off > -(1 << 30) && p->col_off < (1 << 30),
+           MC_ERR_SHAPE, "%s: label offsets out of range", who);
+  g.alpha = p->scale; g.alpha_dev = p->scale_dev;
+  g.sa = p->row_scale_x; g.sb = p->row_scale_y;
+  g.off_r = (int)p->row_off; g.off_c = (int)p->col_off;
+  g.coef_r = p->coef_r; g.coef_c = p->coef_c;
+  return MC_OK;
+}
+}  // namespace
+
+extern "C" size_t mc_ce_fused_fwd_workspace_bytes(int32_t M, int32_t N, int32_t with_columns) {
+  if (M <= 0 || N <= 0) return 0;
+  return fused_fwd_ws(M, N, with_columns != 0, nullptr).bytes;
+}
+
+extern "C" int mc_ce_fused_fwd(const mc_ce_fused_params* p, void* stream) {
+  GemmArgs g;
+  bool aligned;
+  const int rc = fused_common(p, "mc_ce_fused_fwd", g, aligned);
+  if (rc != MC_OK) return rc;
+  MC_CHECK(p->lse_r && p->loss_out, MC_ERR_INVALID, "mc_ce_fused_fwd: null lse_r / loss_out");
+  const bool cols = p->lse_c != nullptr;
+  const FusedWs w = fused_fwd_ws(p->M, p->N, cols, p->workspace);
+  MC_CHECK(p->workspace && aligned16(p->workspace) && p->workspace_bytes >= w.bytes, MC_ERR_WORKSPACE,
+           "mc_ce_fused_fwd: workspace must be >= %zu bytes, 16-B aligned", w.bytes);
+  g.rpart = w.rpart; g.cpart = w.cpart; g.tgt_r = w.tgt_r; g.tgt_c = w.tgt_c;
+  hipStream_t s = (hipStream_t)stream;
+  launch_gemm<1>(g, p->in_dtype, MC_DTYPE_F32, aligned, s);
+  const int nbr = (p->M + 255) / 256, nb = nbr + (cols ? (p->N + 255) / 256 : 0);
+  hipLaunchKernelGGL(ce_fused_reduce_kernel, dim3(nb), dim3(256), 0, s, p->M, p->N, g.tiles_m, g.tiles_n, w.rpart,
+                     w.cpart, w.tgt_r, w.tgt_c, g.off_r, g.off_c, p->coef_r, p->coef_c, p->lse_r, p->lse_c, nbr,
+                     w.partial);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, w.partial, nb, 1.f, nullptr, p->loss_out);
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_ce_fused_fwd: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+extern "C" size_t mc_ce_fused_grad_workspace_bytes(int32_t M, int32_t N) {
+  if (M <= 0 || N <= 0) return 0;
+  return al16((size_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * sizeof(float));
+}
+
+extern "C" int mc_ce_fused_grad(const mc_ce_fused_params* p, void* stream) {
+  GemmArgs g;
+  bool aligned;
+  const int rc = fused_common(p, "mc_ce_fused_grad", g, aligned);
+  if (rc != MC_OK) return rc;
+  MC_CHECK(p->lse_r || p->lse_c, MC_ERR_INVALID, "mc_ce_fused_grad: lse_r and lse_c both NULL");
+  MC_CHECK(p->G, MC_ERR_INVALID, "mc_ce_fused_grad: null G");
+  MC_CHECK(p->g_dtype == MC_DTYPE_F32 || p->g_dtype == MC_DTYPE_BF16, MC_ERR_DTYPE,
+           "mc_ce_fused_grad: G must be fp32 or bf16");
+  MC_CHECK(p->ldg >= p->N, MC_ERR_SHAPE, "mc_ce_fused_grad: ldg < N");
+  const size_t need = mc_ce_fused_grad_workspace_bytes(p->M, p->N);
+  MC_CHECK(!p->dscale_out || (p->workspace && aligned16(p->workspace) && p->workspace_bytes >= need),
+           MC_ERR_WORKSPACE, "mc_ce_fused_grad: workspace must be >= %zu bytes, 16-B aligned", need);
+  g.lse_r = p->lse_r; g.lse_c = p->lse_c; g.gout_dev = p->gout_dev; g.g_times_alpha = p->g_times_scale != 0;
+  g.C = p->G; g.ldc = p->ldg;
+  g.c_vec = aligned16(p->G) && p->ldg % 4 == 0;
+  g.c_vec16 = g.c_vec && p->ldg % 8 == 0;
+  g.gpart = p->dscale_out ? reinterpret_cast<float*>(p->workspace) : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  launch_gemm<2>(g, p->in_dtype, p->g_dtype, aligned, s);
+  if (p->dscale_out)   // sum(G S) / scale: the scale gradient (G here is without gmul)
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, g.gpart, g.tiles_m * g.tiles_n,
+                       p->scale_dev ? 1.f : 1.f / p->scale, p->scale_dev, p->dscale_out);
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_ce_fused_grad: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }

@@ -70,6 +70,20 @@ class GemmNTParams(ctypes.Structure):
     ]
 
 
+class CEFusedParams(ctypes.Structure):
+    """Mirror of ``mc_ce_fused_params`` (include/mc_contrastive.h)."""
+    _fields_ = [
+        ("M", c_i32), ("N", c_i32), ("K", c_i32), ("in_dtype", c_i32),
+        ("X", c_vp), ("ldx", c_i64), ("Y", c_vp), ("ldy", c_i64),
+        ("row_scale_x", c_fp), ("row_scale_y", c_fp),
+        ("scale", ctypes.c_float), ("scale_dev", c_fp),
+        ("row_off", c_i64), ("coef_r", ctypes.c_float), ("col_off", c_i64), ("coef_c", ctypes.c_float),
+        ("lse_r", c_fp), ("lse_c", c_fp), ("loss_out", c_fp), ("gout_dev", c_fp),
+        ("g_dtype", c_i32), ("g_times_scale", c_i32), ("G", c_vp), ("ldg", c_i64),
+        ("dscale_out", c_fp), ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -88,6 +102,10 @@ SYMBOLS = {
     "mc_ce_grad": (ctypes.c_int, [c_i32, c_i32, c_fp, c_i64, c_fp, c_i64, ctypes.c_float, c_fp, c_i64,
                                   ctypes.c_float, c_fp, c_i32, c_vp, c_i64, c_fp, c_fp, c_vp, ctypes.c_size_t, c_vp]),
     "mc_ce_grad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "mc_ce_fused_fwd": (ctypes.c_int, [ctypes.POINTER(CEFusedParams), c_vp]),
+    "mc_ce_fused_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+    "mc_ce_fused_grad": (ctypes.c_int, [ctypes.POINTER(CEFusedParams), c_vp]),
+    "mc_ce_fused_grad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "mc_add_rmsnorm_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_fp, c_fp, ctypes.c_float, c_vp, c_fp, c_fp,
                                           c_vp]),
     "mc_add_rmsnorm_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_fp, c_fp, c_fp, c_fp, c_vp, c_fp, c_fp, c_vp,

@@ -3,9 +3,13 @@
 ``gemm_nt(A, B, alpha)``  C = alpha * A @ B.T on the matrix cores (bf16, fp32 or fp8 e4m3fn in).
 ``quant_rows_fp8(X)``     row-wise amax-scaled e4m3fn quantisation (K padded to 16).
 ``similarity_fp8(I, T, scale)``  scale * I @ T.T through the fp8 MFMA path (config 5).
+``clip_loss_fp8(I, T, scale)``   the symmetric CLIP loss on that fp8 path, logits never stored.
 ``scaled_logits_ce``      autograd op: logits = scale * X @ Y.T, then a weighted
                           sum of row- and/or column-softmax cross-entropies --
-                          the dense part of ClipLoss (loss.py:89-147).
+                          the dense part of ClipLoss (loss.py:89-147) -- fused:
+                          the logits never exist in memory (mc_ce_fused_*).
+``ce_stats`` / ``ce_grad`` the unfused statistics / gradient kernels over a
+                          materialised S (kept for logits the caller needs anyway).
 All launches go on the current HIP stream; nothing synchronises.
 """
 import torch
@@ -87,6 +91,19 @@ def similarity_fp8(image_features, text_features, logit_scale, out_dtype=torch.f
     return gemm_nt(qi, qt, alpha=float(logit_scale), out_dtype=out_dtype, scale_a=si, scale_b=st)
 
 
+def clip_loss_fp8(image_features, text_features, logit_scale):
+    """Symmetric CLIP loss (loss.py:124-147, single process) on fp8 e4m3fn operands, without logits
+    in memory: row-quantised features -> mc_ce_fused_fwd on the fp8 MFMA path (config 5 features,
+    evaluation / frozen-feature scoring; no backward)."""
+    qi, si = quant_rows_fp8(image_features)
+    qt, st = quant_rows_fp8(text_features)
+    n = qi.shape[0]
+    sc = (logit_scale.reshape(()).float() if torch.is_tensor(logit_scale)
+          else torch.tensor(float(logit_scale), device=qi.device)).contiguous()
+    loss, _, _ = ce_fused_fwd(qi, qt, sc, 0, 0.5 / n, 0, 0.5 / n, sx=si, sy=st)
+    return loss
+
+
 def ce_stats(S, axis, label_offset, coef):
     """(lse, weighted NLL sum as a device scalar) along rows (axis 0) or columns (1)."""
     lib = _lib.load()
@@ -118,6 +135,70 @@ def ce_grad(S, lse_r, off_r, coef_r, lse_c, off_c, coef_c, gout, out_dtype, scal
     return G, dscale
 
 
+# G blocks of the fused backward hold at most this many elements (32 MiB bf16):
+# the backward never materialises the full M x N matrix once M * N exceeds it.
+CE_GRAD_BLOCK_ELEMS = 1 << 24
+
+
+def _ce_params(X, Y, sc, row_off, coef_r, col_off, coef_c, sx=None, sy=None):
+    p = _lib.CEFusedParams()
+    p.M, p.K = X.shape
+    p.N = Y.shape[0]
+    p.in_dtype = _lib.dtype_code(X.dtype)
+    p.X, p.ldx, p.Y, p.ldy = X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0)
+    p.row_scale_x, p.row_scale_y = _lib.ptr(sx), _lib.ptr(sy)
+    p.scale_dev = sc.data_ptr()
+    p.row_off, p.coef_r, p.col_off, p.coef_c = int(row_off), float(coef_r), int(col_off), float(coef_c)
+    return p
+
+
+def ce_fused_fwd(X, Y, sc, row_off=0, coef_r=1.0, col_off=0, coef_c=0.0, sx=None, sy=None):
+    """(loss, lse_r, lse_c) of  coef_r * sum_i CE_row_i + coef_c * sum_j CE_col_j,  S = sc * X @ Y^T,
+    computed tile-wise on the matrix cores without storing S (mc_ce_fused_fwd).
+
+    X, Y: row-major (K contiguous) bf16 / fp32, or fp8 e4m3fn with per-row
+    dequantisation factors sx / sy (``quant_rows_fp8``).  sc: 0-d fp32 device
+    tensor.  lse_c is None when coef_c == 0 (no column term)."""
+    lib = _lib.load()
+    M, N = X.shape[0], Y.shape[0]
+    cols = coef_c != 0.0
+    lse_r = torch.empty(M, device=X.device, dtype=torch.float32)
+    lse_c = torch.empty(N, device=X.device, dtype=torch.float32) if cols else None
+    loss = torch.empty((), device=X.device, dtype=torch.float32)
+    p = _ce_params(X, Y, sc, row_off, coef_r, col_off, coef_c, sx, sy)
+    ws_b = lib.mc_ce_fused_fwd_workspace_bytes(M, N, int(cols))
+    ws = _ws(ws_b, X.device)
+    p.lse_r, p.lse_c, p.loss_out = lse_r.data_ptr(), _lib.ptr(lse_c), loss.data_ptr()
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+    _lib.check(lib.mc_ce_fused_fwd(p, _lib.stream_handle(X.device)), "mc_ce_fused_fwd")
+    return loss, lse_r, lse_c
+
+
+def ce_fused_grad(X, Y, sc, lse_r, lse_c, row_off, coef_r, col_off, coef_c, gout, g_dtype, want_dscale=False):
+    """(sc * G, dscale): one block of dloss/dS recomputed from (lse_r, lse_c), S = sc * X @ Y^T
+    (mc_ce_fused_grad); ``G @ Y`` is then dX directly.  dscale is sum(G S) / sc or None."""
+    lib = _lib.load()
+    M, N = X.shape[0], Y.shape[0]
+    G = torch.empty(M, N, device=X.device, dtype=g_dtype)
+    p = _ce_params(X, Y, sc, row_off, coef_r, col_off, coef_c)
+    p.lse_r, p.lse_c = _lib.ptr(lse_r), _lib.ptr(lse_c)
+    p.gout_dev = gout.data_ptr()
+    p.g_dtype, p.g_times_scale, p.G, p.ldg = _lib.dtype_code(g_dtype), 1, G.data_ptr(), N
+    dscale = None
+    ws = None
+    if want_dscale:
+        dscale = torch.empty((), device=X.device, dtype=torch.float32)
+        ws_b = lib.mc_ce_fused_grad_workspace_bytes(M, N)
+        ws = _ws(ws_b, X.device)
+        p.dscale_out, p.workspace, p.workspace_bytes = dscale.data_ptr(), ws.data_ptr(), ws_b
+    _lib.check(lib.mc_ce_fused_grad(p, _lib.stream_handle(X.device)), "mc_ce_fused_grad")
+    return G, dscale
+
+
+def _block_rows(other):
+    return max(128, CE_GRAD_BLOCK_ELEMS // max(other, 1) // 128 * 128)
+
+
 class ScaledLogitsCE(torch.autograd.Function):
     """loss = coef_r * sum_i CE_row_i(S) + coef_c * sum_j CE_col_j(S),  S = scale * X @ Y^T.
 
@@ -125,6 +206,14 @@ class ScaledLogitsCE(torch.autograd.Function):
     coef_c == 0 drops the column term (local-loss halves).  X and Y are the
     (gathered) feature matrices; bf16 inputs run the bf16 MFMA path, fp32
     inputs the exact-fp32 MFMA path; logits and statistics are fp32.
+
+    Neither pass stores S.  Forward: mc_ce_fused_fwd (logit tiles reduced to
+    LSE partials in registers).  Backward: dX in row blocks -- G_blk (recomputed
+    by mc_ce_fused_grad, already times scale) @ Y -- and dY in column blocks
+    from the transposed problem (roles of X/Y, rows/columns, offsets and
+    coefficients swapped) -- G^T_blk @ X; both products are plain NN GEMMs
+    (hipBLASLt), so no operand is ever transposed in memory.  Blocks hold at
+    most CE_GRAD_BLOCK_ELEMS elements.
     """
 
     @staticmethod
@@ -133,28 +222,47 @@ class ScaledLogitsCE(torch.autograd.Function):
         Xc = X.to(dt).contiguous()
         Yc = Y.to(dt).contiguous()
         sc = scale.reshape(()).float().contiguous()
-        S = gemm_nt(Xc, Yc, alpha_dev=sc)
-        lse_r, loss = ce_stats(S, 0, row_off, coef_r)
-        lse_c = None
-        if coef_c != 0.0:
-            lse_c, loss_c = ce_stats(S, 1, col_off, coef_c)
-            loss = loss + loss_c
-        ctx.save_for_backward(Xc, Yc, sc, S, lse_r, lse_c if lse_c is not None else lse_r)
+        loss, lse_r, lse_c = ce_fused_fwd(Xc, Yc, sc, row_off, coef_r, col_off, coef_c)
+        ctx.save_for_backward(Xc, Yc, sc, lse_r, lse_c if lse_c is not None else lse_r)
         ctx.cfg = (row_off, coef_r, col_off, coef_c, lse_c is not None, X.dtype, Y.dtype, scale.dtype, scale.shape)
         return loss
 
     @staticmethod
     def backward(ctx, gout):
-        Xc, Yc, sc, S, lse_r, lse_c = ctx.saved_tensors
+        Xc, Yc, sc, lse_r, lse_c = ctx.saved_tensors
         row_off, coef_r, col_off, coef_c, has_c, xdt, ydt, sdt, sshape = ctx.cfg
-        gdt = Xc.dtype  # G feeds the MFMA GEMMs in the operands' dtype
-        G, dscale = ce_grad(S, lse_r, row_off, coef_r, lse_c if has_c else None, col_off, coef_c, gout, gdt, sc)
-        dX = dY = None
-        if ctx.needs_input_grad[0]:
-            dX = gemm_nt(G, Yc.t().contiguous(), alpha_dev=sc).to(xdt)           # scale * G @ Y
+        lse_c = lse_c if has_c else None
+        gout = gout.reshape(()).float().contiguous()
+        gdt = Xc.dtype  # G feeds the GEMMs in the operands' dtype
+        M, N = Xc.shape[0], Yc.shape[0]
+        want_ds = ctx.needs_input_grad[2]
+        dX = dY = dscale = None
+        if ctx.needs_input_grad[0] or want_ds:
+            dX = torch.empty_like(Xc) if ctx.needs_input_grad[0] else None
+            R = _block_rows(N)
+            parts = []
+            for r0 in range(0, M, R):
+                r1 = min(M, r0 + R)
+                G, ds = ce_fused_grad(Xc[r0:r1], Yc, sc, lse_r[r0:r1], lse_c, row_off + r0, coef_r, col_off - r0,
+                                      coef_c, gout, gdt, want_ds)
+                if dX is not None:
+                    torch.mm(G, Yc, out=dX[r0:r1])
+                if ds is not None:
+                    parts.append(ds)
+            if want_ds:
+                dscale = parts[0] if len(parts) == 1 else torch.stack(parts).sum()
+            dX = dX.to(xdt) if dX is not None else None
         if ctx.needs_input_grad[1]:
-            dY = gemm_nt(G.t().contiguous(), Xc.t().contiguous(), alpha_dev=sc).to(ydt)  # scale * G^T @ X
-        dS = dscale.to(sdt).reshape(sshape) if ctx.needs_input_grad[2] else None
+            dY = torch.empty_like(Yc)
+            R = _block_rows(M)
+            for c0 in range(0, N, R):
+                c1 = min(N, c0 + R)
+                # transposed problem: rows = columns c0..c1 of S, columns = rows of S
+                GT, _ = ce_fused_grad(Yc[c0:c1], Xc, sc, lse_c[c0:c1] if has_c else None, lse_r, col_off + c0,
+                                      coef_c, row_off - c0, coef_r, gout, gdt)
+                torch.mm(GT, Xc, out=dY[c0:c1])
+            dY = dY.to(ydt)
+        dS = dscale.to(sdt).reshape(sshape) if want_ds else None
         return dX, dY, dS, None, None, None, None
 
 

@@ -65,13 +65,39 @@ def test_validation_errors_without_launch():
         _lib.check(lib.mc_scan_fwd(ctypes.byref(p), None), "mc_scan_fwd")
 
 
+def test_fused_ce_validation_without_launch():
+    """mc_ce_fused_fwd / _grad reject bad arguments on the host."""
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    p = _lib.CEFusedParams()
+    p.M, p.N, p.K, p.in_dtype = 4, 4, 8, _lib.MC_DTYPE_BF16
+    assert lib.mc_ce_fused_fwd(ctypes.byref(p), None) == -1 and b"null operand" in lib.mc_last_error()
+    p.X = p.Y = 4096
+    p.in_dtype = 9
+    assert lib.mc_ce_fused_fwd(ctypes.byref(p), None) == -2
+    p.in_dtype, p.row_off = _lib.MC_DTYPE_BF16, 1 << 31
+    assert lib.mc_ce_fused_fwd(ctypes.byref(p), None) == -3
+    p.row_off = 0
+    assert lib.mc_ce_fused_fwd(ctypes.byref(p), None) == -1          # null lse_r / loss_out
+    p.lse_r = p.loss_out = 4096
+    assert lib.mc_ce_fused_fwd(ctypes.byref(p), None) == -5          # no workspace
+    assert lib.mc_ce_fused_grad(ctypes.byref(p), None) == -1         # null G
+    p.lse_r = None
+    assert lib.mc_ce_fused_grad(ctypes.byref(p), None) == -1 and b"both NULL" in lib.mc_last_error()
+    assert lib.mc_ce_fused_fwd_workspace_bytes(8192, 8192, 1) < 8192 * 8192   # O(N^2 / 128), not N^2
+    assert lib.mc_ce_fused_fwd_workspace_bytes(0, 5, 1) == 0
+
+
 @pytest.mark.parametrize("cname,pyname", [("mc_scan_fwd_params", "ScanFwdParams"),
-                                          ("mc_scan_bwd_params", "ScanBwdParams")])
+                                          ("mc_scan_bwd_params", "ScanBwdParams"),
+                                          ("mc_gemm_nt_params", "GemmNTParams"),
+                                          ("mc_ce_fused_params", "CEFusedParams")])
 def test_struct_layout_matches_header(cname, pyname):
     from mamba_clip_amd import _lib
     cls = getattr(_lib, pyname)
     fields = [f for f, _ in cls._fields_]
-    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', "int main(void){",
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', '#include "mc_contrastive.h"',
+           "int main(void){",
            f'printf("size %zu\\n", sizeof({cname}));']
     src += [f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields]
     src += ["return 0;}"]

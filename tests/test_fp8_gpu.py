@@ -113,3 +113,21 @@ def test_clip_model_get_logits_fp8():
     scale = float(m.logit_scale.exp())
     assert (fi - li).abs().max() <= 0.02 * scale
     torch.testing.assert_close(ft, fi.T)
+
+
+@pytest.mark.parametrize("n,E", [(256, 512), (8192, 512)])
+def test_clip_loss_fp8_fused_matches_oracle(n, E):
+    """Fused fp8 logits + CE (no logits in memory) vs fp64 CE over the exact dequantised product
+    (similarity_fp8_ref), and within the fp8 bound of the fp64 loss on the unquantised features."""
+    from mamba_clip_amd.ops import clip_loss_fp8
+    g = torch.Generator().manual_seed(n)
+    I = F.normalize(torch.randn(n, E, generator=g), dim=-1)
+    T = F.normalize(I + 0.5 * torch.randn(n, E, generator=g), dim=-1)
+    scale = 50.0
+    got = float(clip_loss_fp8(I.to(DEV), T.to(DEV), torch.tensor(scale, device=DEV)))
+    S = similarity_fp8_ref(I, T, scale)
+    lab = torch.arange(n)
+    want = float((F.cross_entropy(S, lab) + F.cross_entropy(S.T, lab)) / 2)
+    assert abs(got - want) <= 1e-5 * abs(want) + 1e-6, (got, want)
+    l_ref = float(clip_loss(I.double(), T.double(), torch.tensor(scale, dtype=torch.float64)))
+    assert abs(got - l_ref) <= 5e-3 * abs(l_ref)

@@ -147,3 +147,96 @@ def test_local_loss_matches_reference_gloo_golden(world):
         torch.testing.assert_close(img.grad.cpu(), g[f"{key}.grad_img"], rtol=1e-4, atol=1e-6)
         torch.testing.assert_close(txt.grad.cpu(), g[f"{key}.grad_txt"], rtol=1e-4, atol=1e-6)
         torch.testing.assert_close(s.grad.cpu().reshape(1), g[f"{key}.grad_scale"], rtol=1e-4, atol=1e-6)
+
+
+# ---------------------------------------------------------------- fused logits + CE (mc_ce_fused_*)
+@pytest.mark.parametrize("M,N,E,coef_c,dtype", [(1000, 1000, 64, 0.5 / 1000, torch.float32),
+                                               (300, 1100, 96, 0.0, torch.float32),
+                                               (640, 640, 128, 0.5 / 640, torch.bfloat16)])
+def test_fused_ce_blocked_backward(monkeypatch, M, N, E, coef_c, dtype):
+    """Force several G blocks per pass (row blocks for dX, column blocks for dY with the transposed
+    problem) and check loss / dX / dY / d(scale) against fp64, with label offsets on both axes."""
+    from mamba_clip_amd import ops
+    monkeypatch.setattr(ops, "CE_GRAD_BLOCK_ELEMS", 128 * 256)
+    g = torch.Generator().manual_seed(M + N)
+    X = torch.nn.functional.normalize(torch.randn(M, E, generator=g), dim=-1).to(dtype)
+    Y = torch.nn.functional.normalize(torch.randn(N, E, generator=g), dim=-1).to(dtype)
+    roff = (N - M) // 2
+    coff = 0
+    xr, yr = X.double().requires_grad_(True), Y.double().requires_grad_(True)
+    sr = torch.tensor(20.0, dtype=torch.float64, requires_grad=True)
+    ref = _ce_oracle(xr, yr, sr, roff, 0.5 / M, coff, coef_c)
+    ref.backward()
+    xd, yd = X.to(DEV).requires_grad_(True), Y.to(DEV).requires_grad_(True)
+    sd = torch.tensor(20.0, device=DEV, requires_grad=True)
+    loss = ops.scaled_logits_ce(xd, yd, sd, roff, 0.5 / M, coff, coef_c)
+    loss.backward()
+    tol = 1e-5 if dtype == torch.float32 else 1e-3
+    assert abs(float(loss) - float(ref)) <= tol * abs(float(ref)) + 1e-6
+    for got, want in ((xd.grad, xr.grad), (yd.grad, yr.grad)):
+        scale = float(want.abs().max())
+        err = float((got.double().cpu() - want).abs().max())
+        assert err <= (1e-5 if dtype == torch.float32 else 1e-2) * scale, (err, scale)
+    assert abs(float(sd.grad) - float(sr.grad)) <= tol * abs(float(sr.grad)) + 1e-5
+
+
+def test_fused_ce_no_n_by_n_allocation_c5_size():
+    """N = 8192 (config 5's global batch), bf16: forward + backward never allocate an N x N buffer
+    (peak growth stays below one bf16 N x N matrix), and the loss / lse agree with the unfused
+    kernels over a materialised S."""
+    from mamba_clip_amd.ops import ce_fused_fwd, ce_stats, gemm_nt, scaled_logits_ce
+    N, E = 8192, 512
+    g = torch.Generator().manual_seed(5)
+    img = torch.nn.functional.normalize(torch.randn(N, E, generator=g), dim=-1).bfloat16().to(DEV)
+    txt = torch.nn.functional.normalize(torch.randn(N, E, generator=g), dim=-1).bfloat16().to(DEV)
+    s = torch.tensor(30.0, device=DEV, requires_grad=True)
+    i_d, t_d = img.clone().requires_grad_(True), txt.clone().requires_grad_(True)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    loss = scaled_logits_ce(i_d, t_d, s, 0, 0.5 / N, 0, 0.5 / N)
+    loss.backward()
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert peak < N * N * 2, f"peak {peak / 2**20:.1f} MiB >= one bf16 N x N"
+    # unfused reference on the same device: S materialised once, row / column stats
+    S = gemm_nt(img, txt, alpha_dev=s.detach())
+    lr, l_r = ce_stats(S, 0, 0, 0.5 / N)
+    lc, l_c = ce_stats(S, 1, 0, 0.5 / N)
+    l2, lse_r, lse_c = ce_fused_fwd(img, txt, s.detach(), 0, 0.5 / N, 0, 0.5 / N)
+    torch.testing.assert_close(lse_r, lr, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(lse_c, lc, rtol=1e-6, atol=1e-5)
+    assert abs(float(l2) - float(l_r + l_c)) <= 1e-5 * float(l_r + l_c)
+    assert abs(float(loss) - float(l2)) <= 1e-6 * float(l2)
+    assert torch.isfinite(i_d.grad).all() and torch.isfinite(t_d.grad).all()
+
+
+def test_unfused_ce_kernels_match_fp64():
+    """mc_ce_stats / mc_ce_grad over a materialised S (rows and columns, label offsets)."""
+    from mamba_clip_amd.ops import ce_grad, ce_stats
+    g = torch.Generator().manual_seed(3)
+    S = (torch.randn(70, 300, generator=g) * 8).double()
+    lr_ref = torch.logsumexp(S, 1)
+    lc_ref = torch.logsumexp(S, 0)
+    Sd = S.float().to(DEV)
+    lr, loss_r = ce_stats(Sd, 0, 11, 0.25)
+    lc, loss_c = ce_stats(Sd, 1, -5, 0.5)
+    torch.testing.assert_close(lr.cpu().double(), lr_ref, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(lc.cpu().double(), lc_ref, rtol=1e-6, atol=1e-5)
+    r = torch.arange(70)
+    c = torch.arange(300)
+    want_r = 0.25 * (lr_ref - S[r, r + 11]).sum()
+    ok = (c - 5 >= 0) & (c - 5 < 70)
+    want_c = 0.5 * (lc_ref - torch.where(ok, S[(c - 5).clamp(0, 69), c], torch.zeros(300, dtype=S.dtype))).sum()
+    assert abs(float(loss_r) - float(want_r)) <= 1e-5 * abs(float(want_r))
+    assert abs(float(loss_c) - float(want_c)) <= 1e-5 * abs(float(want_c))
+    sc = torch.tensor(2.0, device=DEV)
+    G, ds = ce_grad(Sd, lr, 11, 0.25, lc, -5, 0.5, torch.tensor(1.5, device=DEV), torch.float32, sc)
+    P_r = torch.softmax(S, 1)
+    P_c = torch.softmax(S, 0)
+    Gr = 0.25 * (P_r - torch.nn.functional.one_hot(r + 11, 300).double())
+    oh_c = torch.zeros(70, 300, dtype=torch.float64)
+    oh_c[(c - 5)[ok], c[ok]] = 1
+    Gw = 1.5 * (Gr + 0.5 * (P_c - oh_c))
+    torch.testing.assert_close(G.cpu().double(), Gw, rtol=1e-5, atol=1e-6)
+    assert abs(float(ds) - float((Gw * S).sum() / 2.0)) <= 1e-4 * abs(float((Gw * S).sum() / 2.0)) + 1e-5
