@@ -93,6 +93,17 @@ typedef struct mc_scan_fwd_params {
    * Not needed for training: mc_scan_bwd recomputes y for dz. */
   void* out_y;
   int64_t out_y_batch_stride, out_y_dim_stride;
+  /* Grouped directions (SS2D's cross-scan, reference model.py:510-517, merged
+   * at 553-565), both 0 = off:
+   * reverse_groups  bitmask: group g scans its sequence backwards -- step l
+   *                 reads and writes every per-position tensor (u, delta, B, C,
+   *                 out) at position seqlen-1-l -- so a flipped direction needs
+   *                 no flipped copy of its inputs or outputs;
+   * u_groups        k > 0: u holds k blocks of dim/n_groups channel rows and
+   *                 group g reads block g % k (SS2D: 4 directions share the 2
+   *                 blocks [x, x^T]); 0 = u has dim rows as usual.
+   * Either set: z must be NULL (the cross-scan has no gate). */
+  int32_t reverse_groups, u_groups;
 } mc_scan_fwd_params;
 
 typedef struct mc_scan_bwd_params {
@@ -138,6 +149,11 @@ typedef struct mc_scan_bwd_params {
    * output y + D u that dz = dout * y * silu'(z) needs from the chunk states */
   const void* out_y;
   int64_t out_y_batch_stride, out_y_dim_stride;
+  /* reverse_groups / u_groups as in mc_scan_fwd_params (same values as the
+   * forward).  dout, du, ddelta, dB, dC follow the same mirrored positions; with
+   * u_groups > 0, du still has dim rows (one per group and channel): the caller
+   * sums the groups that share a u block. */
+  int32_t reverse_groups, u_groups;
 } mc_scan_bwd_params;
 
 /* number of MC_SCAN_CHUNK-long chunks covering seqlen */

@@ -107,8 +107,56 @@ __device__ __forceinline__ void st16_masked(T* __restrict__ p, const uint4& q, i
     }
   }
 }
+
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void st16(void* p, const uint4& q) { *reinterpret_cast<uint4*>(p) = q; }
+
+// Mirrored sequence access for reversed scan groups (SS2D's flipped directions,
+// reference model.py:510-517 / 553-565).  A reversed group's chunk of steps
+// [l0, l0 + kT) lives at positions [L - l0 - kT, L - l0): lane c of a row moves
+// the 16-B block at ascending position cm = L - l0 - kT + c * VI (addresses
+// keep increasing with the lane, so the accesses coalesce like a forward walk)
+// and the block holds the steps of block kVPR - 1 - c in reverse element order.
+// ld16_top: that block in MEMORY order (the caller flips it where the values are
+// consumed -- flipping right after the load would make the wave wait for it);
+// only its top nvalid elements (the steps < L) exist, the rest read as 0.
+// st16_rev: step-ordered values -> the block, flipped, top nvalid elements.
+// Whole aligned blocks move as one 16-B access, others element by element.
+__device__ __forceinline__ uint32_t swap16(uint32_t w) { return (w >> 16) | (w << 16); }
+template <typename T>
+__device__ __forceinline__ uint4 reverse_elems(const uint4& q) {
+  if constexpr (sizeof(T) == 4) return make_uint4(q.w, q.z, q.y, q.x);
+  else return make_uint4(swap16(q.w), swap16(q.z), swap16(q.y), swap16(q.x));
+}
+template <typename T>
+__device__ __forceinline__ uint4 ld16_top(const T* __restrict__ row, int cm, int nvalid) {
+  constexpr int N = ElemTraits<T>::kVec;
+  if (nvalid == N && ((reinterpret_cast<uintptr_t>(row + cm) & 15) == 0)) return ld16(row + cm);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t b = (i >= N - nvalid) ? ld_bits(row + (cm + i)) : 0u;
+    if constexpr (sizeof(T) == 4) w[i] = b;
+    else w[i >> 1] |= b << (16 * (i & 1));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <typename T>
+__device__ __forceinline__ void st16_rev(T* __restrict__ row, int cm, const uint4& q, int nvalid) {
+  constexpr int N = ElemTraits<T>::kVec;
+  if (nvalid == N && ((reinterpret_cast<uintptr_t>(row + cm) & 15) == 0)) {
+    st16(row + cm, reverse_elems<T>(q));
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i < nvalid) {
+      T* p = row + (cm + N - 1 - i);
+      if constexpr (sizeof(T) == 4) st_bits(p, word_of(q, i));
+      else st_bits(p, (word_of(q, i >> 1) >> (16 * (i & 1))) & 0xffffu);
+    }
+  }
+}
 
 // ---------------------------------------------------------------- raw buffer access
 // A buffer resource (V#) holds a wave-uniform base and byte range in SGPRs, so

@@ -58,6 +58,7 @@ struct BwdArgs {
   float* slab_a;                     // [b][kN][dim] (dA partials, one owner per element)
   float* slab_d;                     // [b][dim]
   float* slab_bias;                  // [b][dim]
+  int rev_groups, u_groups;          // grouped directions (0 = off; element-wise path only)
 };
 
 __device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
@@ -188,7 +189,11 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
   const TI* src1 = reinterpret_cast<const TI*>(wave == 0 ? a.delta : a.dout);
   const int64_t bs0 = wave == 0 ? a.u_bs : (hasZ ? a.z_bs : a.go_bs), ds0 = wave == 0 ? a.u_ds : (hasZ ? a.z_ds : a.go_ds);
   const int64_t bs1 = wave == 0 ? a.dt_bs : a.go_bs, ds1 = wave == 0 ? a.dt_ds : a.go_ds;
-  const TI* rb0 = src0 + (int64_t)b * bs0 + (int64_t)dbase * ds0;
+  // grouped directions: reversed groups walk mirrored positions; u_groups > 0 shares u blocks
+  // (vector path: the host guarantees seqlen % VI == 0, so a mirrored 16-B block is aligned)
+  const bool rev = (a.rev_groups >> g) & 1;
+  const int row0 = (a.u_groups && wave == 0) ? (g % a.u_groups) * H + dblk * kRows : dbase;
+  const TI* rb0 = src0 + (int64_t)b * bs0 + (int64_t)row0 * ds0;
   const TI* rb1 = src1 + (int64_t)b * bs1 + (int64_t)dbase * ds1;
   const int slot0 = wave == 0 ? 0 : 2, slot1 = wave == 0 ? 1 : 3;
   const bool stage0 = wave == 0 || hasZ;     // wave 1 without z stages dout only
@@ -238,14 +243,24 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
       const int col0 = l0 + cc * VI;
       if constexpr (kAligned) {
         // chunk -1: an offset past every buffer range reads 0 (no branch around the loads)
-        const uint32_t o0 = valid ? (uint32_t)(r * ds0 + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
-        const uint32_t o1 = valid ? (uint32_t)(r * ds1 + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
-        pf0[k] = buf_ld16(rs0, o0);
-        pf1[k] = buf_ld16(rs1, o1);
+        // reversed group: ascending mirrored block (mc_common.h ld16_rev; a block past the end
+        // reads an unused neighbour or wraps out of range; steps >= L are zeroed before use)
+        const int cm = rev ? L_ - l0 - kTC + cc * VI : col0;
+        const uint32_t o0 = valid ? (uint32_t)(r * ds0 + cm) * (uint32_t)sizeof(TI) : 0x80000000u;
+        const uint32_t o1 = valid ? (uint32_t)(r * ds1 + cm) * (uint32_t)sizeof(TI) : 0x80000000u;
+        pf0[k] = buf_ld16(rs0, o0);   // (reversed groups: element order flipped at staging, not here --
+        pf1[k] = buf_ld16(rs1, o1);   //  touching the values would wait for the loads)
       } else {
-        const int nv = valid ? max(0, min(VI, L_ - col0)) : 0;
-        pf0[k] = ld16_masked(rb0 + (int64_t)r * ds0 + (valid ? col0 : 0), nv);
-        pf1[k] = ld16_masked(rb1 + (int64_t)r * ds1 + (valid ? col0 : 0), nv);
+        if (rev) {
+          const int nvr = valid ? max(0, min(VI, L_ - (l0 + (VPR - 1 - cc) * VI))) : 0;
+          const int cm = valid ? L_ - l0 - kTC + cc * VI : 0;
+          pf0[k] = ld16_top(rb0 + (int64_t)r * ds0, cm, nvr);   // flipped at staging
+          pf1[k] = ld16_top(rb1 + (int64_t)r * ds1, cm, nvr);
+        } else {
+          const int nv = valid ? max(0, min(VI, L_ - col0)) : 0;
+          pf0[k] = ld16_masked(rb0 + (int64_t)r * ds0 + (valid ? col0 : 0), nv);
+          pf1[k] = ld16_masked(rb1 + (int64_t)r * ds1 + (valid ? col0 : 0), nv);
+        }
       }
     }
 #pragma unroll
@@ -275,9 +290,10 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < VPR; ++k) {
       const int j = lane + k * kRows;
-      const int off = CR::off(j / VPR, j % VPR);
-      if (stage0) *reinterpret_cast<uint4*>(rows + slot0 * CR::kBytes + off) = pf0[k];
-      *reinterpret_cast<uint4*>(rows + slot1 * CR::kBytes + off) = pf1[k];
+      const int off = CR::off(j / VPR, rev ? VPR - 1 - j % VPR : j % VPR);   // reversed: mirrored block
+      // mirrored blocks arrive in memory order: flip them here
+      if (stage0) *reinterpret_cast<uint4*>(rows + slot0 * CR::kBytes + off) = rev ? reverse_elems<TI>(pf0[k]) : pf0[k];
+      *reinterpret_cast<uint4*>(rows + slot1 * CR::kBytes + off) = rev ? reverse_elems<TI>(pf1[k]) : pf1[k];
     }
 #pragma unroll
     for (int k = 0; k < kQPer; ++k) {
@@ -544,14 +560,18 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
         for (int k = 0; k < VPR; ++k) {
           const int j = lane + k * kRows;
           const int r = j / VPR, cc = j % VPR;
+          const int cl = rev ? VPR - 1 - cc : cc;     // LDS block of this lane's vector
           const int col0 = l0 + cc * VI;
-          if (r < nrows && col0 < L_) {
-            const uint4 v = *reinterpret_cast<const uint4*>(rows + slot * CR::kBytes + CR::off(r, cc));
-            const int nv = min(VI, L_ - col0);
+          const int cm = L_ - l0 - kTC + cc * VI;      // (reversed) ascending mirrored position
+          if (r < nrows && l0 + cl * VI < L_) {
+            const uint4 v = *reinterpret_cast<const uint4*>(rows + slot * CR::kBytes + CR::off(r, cl));
+            const int nv = min(VI, L_ - (l0 + cl * VI));
             if constexpr (kAligned) {
-              const uint32_t o = (uint32_t)(r * ds + col0) * (uint32_t)sizeof(TI);
-              if (nv == VI) buf_st16(rso, o, v);
-              else buf_st16_masked<TI>(rso, o, v, nv);
+              const uint32_t o = (uint32_t)(r * ds + (rev ? cm : col0)) * (uint32_t)sizeof(TI);
+              if (nv == VI) buf_st16(rso, o, rev ? reverse_elems<TI>(v) : v);
+              else buf_st16_masked<TI>(rso, o, v, nv);   // (never with rev: seqlen % VI == 0)
+            } else if (rev) {
+              st16_rev(base + (int64_t)r * ds, cm, v, nv);
             } else {
               st16_masked(base + (int64_t)r * ds + col0, v, nv);
             }
@@ -585,7 +605,7 @@ template <typename TW, int kN>
 __global__ __launch_bounds__(256) void bc_quad_kernel(const TW* __restrict__ B, const TW* __restrict__ C,
                                                       int64_t B_bs, int64_t B_gs, int64_t B_ns, int64_t C_bs,
                                                       int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
-                                                      f32x4* __restrict__ out) {
+                                                      int rev, f32x4* __restrict__ out) {
   constexpr int kP = kN / 2;
   const int64_t total = (int64_t)batch * G * L * kP;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -594,8 +614,9 @@ __global__ __launch_bounds__(256) void bc_quad_kernel(const TW* __restrict__ B, 
     const int l = (int)(rest % L);
     const int64_t bg = rest / L;
     const int gg = (int)(bg % G), bb = (int)(bg / G);
-    const TW* bs = B + (int64_t)bb * B_bs + (int64_t)gg * B_gs + l;
-    const TW* cs = C + (int64_t)bb * C_bs + (int64_t)gg * C_gs + l;
+    const int ls = ((rev >> gg) & 1) ? L - 1 - l : l;   // reversed groups: mirrored positions
+    const TW* bs = B + (int64_t)bb * B_bs + (int64_t)gg * B_gs + ls;
+    const TW* cs = C + (int64_t)bb * C_bs + (int64_t)gg * C_gs + ls;
     const int n0 = 2 * p;
     f32x4 v;
     v.x = n0 < dstate ? to_f(bs[(int64_t)n0 * B_ns]) : 0.f;
@@ -615,7 +636,7 @@ static hipError_t launch_bc_quads(const mc_scan_bwd_params* p, int np, f32x4* ou
 #define MC_BCQ(NP)                                                                                                 \
   hipLaunchKernelGGL((bc_quad_kernel<TW, NP>), grid, 256, 0, s, B, C, p->B_batch_stride, p->B_group_stride,       \
                      p->B_dstate_stride, p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch,      \
-                     p->n_groups, p->seqlen, p->dstate, out)
+                     p->n_groups, p->seqlen, p->dstate, p->reverse_groups, out)
   if (np == 8) MC_BCQ(8);
   else if (np == 16) MC_BCQ(16);
   else MC_BCQ(32);
@@ -626,7 +647,8 @@ static hipError_t launch_bc_quads(const mc_scan_bwd_params* p, int np, f32x4* ou
 // dB / dC: sum the per-workgroup slabs; dA / dD / dbias: sum the per-batch slabs.
 template <typename TW, int kN>
 __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, int G, int nblk,
-                                                           int dstate, int L, TW* __restrict__ dB, TW* __restrict__ dC) {
+                                                           int dstate, int L, int rev, TW* __restrict__ dB,
+                                                           TW* __restrict__ dC) {
   // thread -> (b*G+g, l, which, n), n fastest: the slab reads are coalesced
   const int64_t total = (int64_t)batch * G * L * 2 * kN;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -640,7 +662,8 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
     float s = 0.f;
     for (int k = 0; k < nblk; ++k) s += slab[((bgi * nblk + k) * L + l) * (2 * kN) + which * kN + n];
     TW* dst = which ? dC : dB;
-    dst[(bgi * dstate + n) * L + l] = from_f<TW>(s);
+    const int lo = ((rev >> (int)(bgi % G)) & 1) ? L - 1 - l : l;
+    dst[(bgi * dstate + n) * L + lo] = from_f<TW>(s);
   }
 }
 
@@ -744,7 +767,8 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
   const int64_t total = (int64_t)a.batch * a.n_groups * kN * 2 * a.seqlen;
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL((scan_bwd_reduce_bc<TW, kN>), dim3(grid), dim3(256), 0, s, a.slab_bc, a.batch, a.n_groups,
-                     a.nblk, a.dstate, a.seqlen, reinterpret_cast<TW*>(dB), reinterpret_cast<TW*>(dC));
+                     a.nblk, a.dstate, a.seqlen, a.rev_groups, reinterpret_cast<TW*>(dB),
+                     reinterpret_cast<TW*>(dC));
   // slab_a is [b][n][d]: column c = n * dim + d -> dA[d][n] (transposed on output)
   const int ca = a.dim * a.dstate;
   hipLaunchKernelGGL(scan_bwd_colsum_nd, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, a.dim, a.dstate,
@@ -801,6 +825,14 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
                (int64_t)p->seqlen * 2 * np * 4 < ((int64_t)1 << 31),
            MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit offsets", p->seqlen);
   MC_CHECK(p->chunk_states, MC_ERR_INVALID, "mc_scan_bwd: chunk_states (from the training forward) required");
+  const bool dirs = p->reverse_groups != 0 || p->u_groups != 0;
+  if (dirs) {
+    MC_CHECK(!p->z && p->u_groups >= 0 && p->u_groups <= p->n_groups && p->n_groups <= 31 &&
+                 (p->reverse_groups >> p->n_groups) == 0,
+             MC_ERR_SHAPE, "mc_scan_bwd: reverse_groups / u_groups need no z, 0 <= u_groups <= n_groups <= 31 and "
+             "a mask within n_groups (got mask 0x%x, u_groups %d, n_groups %d)", p->reverse_groups, p->u_groups,
+             p->n_groups);
+  }
   const BwdWs w = bwd_ws_layout(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups);
   MC_CHECK(p->workspace && p->workspace_bytes >= w.total && (reinterpret_cast<uintptr_t>(p->workspace) & 255) == 0,
            MC_ERR_WORKSPACE, "mc_scan_bwd: workspace must be >= %zu bytes and 256-B aligned (got %zu)", w.total,
@@ -835,6 +867,7 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   a.slab_a = reinterpret_cast<float*>(ws + w.slab_a);
   a.slab_d = reinterpret_cast<float*>(ws + w.slab_d);
   a.slab_bias = reinterpret_cast<float*>(ws + w.slab_bias);
+  a.rev_groups = dirs ? p->reverse_groups : 0; a.u_groups = dirs ? p->u_groups : 0;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
@@ -852,7 +885,7 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
                      span_ok(p->z, p->z_dim_stride) && span_ok(p->dout, p->dout_dim_stride) &&
                      span_ok(p->du, p->du_dim_stride) && span_ok(p->ddelta, p->ddelta_dim_stride) &&
                      span_ok(p->dz, p->dz_dim_stride);
-  aligned = aligned && spans;
+  aligned = aligned && spans && (!dirs || p->seqlen % (16 / ib) == 0);   // mirrored blocks stay aligned
   if (p->itype == MC_DTYPE_F32) rc = launch_bwd_t<float>(a, aligned, s);
   else if (p->itype == MC_DTYPE_BF16) rc = launch_bwd_t<bf16_t>(a, aligned, s);
   else rc = launch_bwd_t<f16_t>(a, aligned, s);

@@ -53,7 +53,7 @@ template <typename TW, int kNp>
 __global__ __launch_bounds__(256) void bc_relayout_kernel(const TW* __restrict__ B, const TW* __restrict__ C,
                                                          int64_t B_bs, int64_t B_gs, int64_t B_ns, int64_t C_bs,
                                                          int64_t C_gs, int64_t C_ns, int batch, int G, int L,
-                                                         int dstate, float* __restrict__ out) {
+                                                         int dstate, int rev, float* __restrict__ out) {
   const int64_t total = (int64_t)batch * G * L * 2 * kNp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int j = (int)(i % (2 * kNp));
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void bc_relayout_kernel(const TW* __restrict__
     if (n < dstate) {
       const TW* src = isC ? C + (int64_t)b * C_bs + (int64_t)g * C_gs + (int64_t)n * C_ns
                           : B + (int64_t)b * B_bs + (int64_t)g * B_gs + (int64_t)n * B_ns;
-      v = to_f(src[l]);
+      v = to_f(src[((rev >> g) & 1) ? L - 1 - l : l]);   // reversed groups: mirrored positions
     }
     out[i] = v;
   }
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void bc_relayout_kernel(const TW* __restrict__
 template <typename TW>
 inline hipError_t launch_bc_relayout(const void* B, const void* C, int64_t B_bs, int64_t B_gs, int64_t B_ns,
                                      int64_t C_bs, int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
-                                     float* out, hipStream_t s) {
+                                     int rev, float* out, hipStream_t s) {
   const int np = padded_dstate(dstate);
   const int64_t total = (int64_t)batch * G * L * 2 * np;
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
@@ -84,24 +84,24 @@ inline hipError_t launch_bc_relayout(const void* B, const void* C, int64_t B_bs,
   const TW* c = reinterpret_cast<const TW*>(C);
   if (np == 8)
     hipLaunchKernelGGL((bc_relayout_kernel<TW, 8>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch,
-                       G, L, dstate, out);
+                       G, L, dstate, rev, out);
   else if (np == 16)
     hipLaunchKernelGGL((bc_relayout_kernel<TW, 16>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns,
-                       batch, G, L, dstate, out);
+                       batch, G, L, dstate, rev, out);
   else
     hipLaunchKernelGGL((bc_relayout_kernel<TW, 32>), grid, 256, 0, s, b, c, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns,
-                       batch, G, L, dstate, out);
+                       batch, G, L, dstate, rev, out);
   return hipGetLastError();
 }
 
 inline hipError_t relayout_bc(int wtype, const void* B, const void* C, int64_t B_bs, int64_t B_gs, int64_t B_ns,
                               int64_t C_bs, int64_t C_gs, int64_t C_ns, int batch, int G, int L, int dstate,
-                              float* out, hipStream_t s) {
+                              int rev, float* out, hipStream_t s) {
   if (wtype == MC_DTYPE_F32)
-    return launch_bc_relayout<float>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
+    return launch_bc_relayout<float>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, rev, out, s);
   if (wtype == MC_DTYPE_BF16)
-    return launch_bc_relayout<bf16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
-  return launch_bc_relayout<f16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, out, s);
+    return launch_bc_relayout<bf16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, rev, out, s);
+  return launch_bc_relayout<f16_t>(B, C, B_bs, B_gs, B_ns, C_bs, C_gs, C_ns, batch, G, L, dstate, rev, out, s);
 }
 
 // LDS row of one channel for one chunk: kT / VI blocks; block k = {u vector k

@@ -39,6 +39,7 @@ struct FwdArgs {
   const float* D; const void* z; const float* delta_bias;
   void* out; float* chunk_states; float* last_state;
   void* out_y; int64_t y_bs, y_ds;   // nullable: pre-gate y + D u (training with z: the backward's dz input)
+  int rev_groups, u_groups;          // grouped directions (0 = off; element-wise path only)
 };
 
 // Variants (template knobs, chosen on the host):
@@ -76,16 +77,20 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   const bool softplus = a.softplus != 0;
 
   const TI* __restrict__ u = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs;
+  // grouped directions: reversed groups walk mirrored positions; u_groups > 0 shares u blocks
+  // (vector modes: the host guarantees seqlen % VI == 0, so a mirrored 16-B block is aligned)
+  const bool rev = (a.rev_groups >> g) & 1;
+  const int urow0 = a.u_groups ? (g % a.u_groups) * H + dblk * kRows : dbase;
   const TI* __restrict__ dl = reinterpret_cast<const TI*>(a.delta) + (int64_t)b * a.dt_bs;
   const TI* __restrict__ zp = reinterpret_cast<const TI*>(a.z) + (int64_t)b * a.z_bs;
   TI* __restrict__ out = reinterpret_cast<TI*>(a.out) + (int64_t)b * a.o_bs;
   // (whole-chunk mode) this wave's rows of u / delta / z / out as buffer ranges: 32-bit offsets
-  auto rows_rsrc = [&](const void* base, int64_t ds) {
-    return make_rsrc(reinterpret_cast<const TI*>(base) + (int64_t)dbase * ds,
+  auto rows_rsrc = [&](const void* base, int64_t ds, int row0 = -1) {
+    return make_rsrc(reinterpret_cast<const TI*>(base) + (int64_t)(row0 < 0 ? dbase : row0) * ds,
                      (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)));
   };
   const __amdgpu_buffer_rsrc_t rs_out = rows_rsrc(out, a.o_ds);
-  const __amdgpu_buffer_rsrc_t rs_u = rows_rsrc(u, a.u_ds), rs_d = rows_rsrc(dl, a.dt_ds);
+  const __amdgpu_buffer_rsrc_t rs_u = rows_rsrc(u, a.u_ds, urow0), rs_d = rows_rsrc(dl, a.dt_ds);
   const __amdgpu_buffer_rsrc_t rs_z = rows_rsrc(hasZ ? (const void*)zp : (const void*)u, hasZ ? a.z_ds : a.u_ds);
   const __amdgpu_buffer_rsrc_t rs_y =
       rows_rsrc(a.out_y ? (const void*)(reinterpret_cast<const TI*>(a.out_y) + (int64_t)b * a.y_bs) : (const void*)u,
@@ -152,11 +157,22 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
       const int rr = min(r, nrows - 1);   // rows past the group end: load a valid row, never stored
       const int col0 = l0 + c * VI;
       if constexpr (kAligned == 2) {   // 32-bit offsets into the wave's row block (no 64-bit pointers)
-        pu[k] = buf_ld16(rs_u, (uint32_t)(rr * a.u_ds + col0) * (uint32_t)sizeof(TI));
-        pd[k] = buf_ld16(rs_d, (uint32_t)(rr * a.dt_ds + col0) * (uint32_t)sizeof(TI));
+        // reversed group: ascending mirrored block (mc_common.h ld16_rev; past the end it goes
+        // negative -> wraps out of range for row 0, reads an unused neighbour otherwise: never consumed)
+        const int cm = rev ? L_ - l0 - kT + c * VI : col0;
+        // (element order is reversed at staging: touching the values here would wait for the loads)
+        pu[k] = buf_ld16(rs_u, (uint32_t)(rr * a.u_ds + cm) * (uint32_t)sizeof(TI));
+        pd[k] = buf_ld16(rs_d, (uint32_t)(rr * a.dt_ds + cm) * (uint32_t)sizeof(TI));
         continue;
       }
-      const TI* su = u + (int64_t)(dbase + rr) * a.u_ds + col0;
+      if (rev) {
+        const int nv = max(0, min(VI, L_ - (l0 + (kVPR - 1 - c) * VI)));   // steps < L of block kVPR-1-c
+        const int cm = L_ - l0 - kT + c * VI;
+        pu[k] = ld16_top(u + (int64_t)(urow0 + rr) * a.u_ds, cm, nv);   // flipped at staging
+        pd[k] = ld16_top(dl + (int64_t)(dbase + rr) * a.dt_ds, cm, nv);
+        continue;
+      }
+      const TI* su = u + (int64_t)(urow0 + rr) * a.u_ds + col0;
       const TI* sd = dl + (int64_t)(dbase + rr) * a.dt_ds + col0;
       if (full) {
         pu[k] = ld16(su);
@@ -181,9 +197,9 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
     for (int k = 0; k < kVPR; ++k) {
       const int j = lane + k * kRows;
       const int r = j / kVPR, c = j % kVPR;
-      char* blk = rowbuf + r * RL::kStride + c * RL::kBlock;
-      st16(blk, pu[k]);
-      st16(blk + 16, pd[k]);
+      char* blk = rowbuf + r * RL::kStride + (rev ? kVPR - 1 - c : c) * RL::kBlock;   // reversed: mirrored block
+      st16(blk, rev ? reverse_elems<TI>(pu[k]) : pu[k]);        // mirrored blocks arrive in memory order
+      st16(blk + 16, rev ? reverse_elems<TI>(pd[k]) : pd[k]);
     }
     {
       float4 cur[kBCPer];
@@ -313,14 +329,16 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
     for (int k = 0; k < kVPR; ++k) {
       const int j = lg + k * kRows;
       const int r = j / kVPR, c = j % kVPR;
+      const int cl = rev ? kVPR - 1 - c : c;          // LDS block of this lane's vector
       const int col0 = l0 + c * VI;
-      const int nv = max(0, min(VI, L_ - col0));
+      const int cm = L_ - l0 - kT + c * VI;            // (reversed) ascending mirrored position
+      const int nv = max(0, min(VI, L_ - (l0 + cl * VI)));
       float o[VI];
       // y of step s (within the chunk) lives in group s / kG: first half of the
       // group's y values at the u bytes, second half at the delta bytes.
 #pragma unroll
       for (int e = 0; e < VI; ++e) {
-        const int st = c * VI + e;
+        const int st = cl * VI + e;
         const int g0 = st - st % kG;
         const int ie = st % kG;
         const char* pu = rowbuf + r * RL::kStride + (g0 / VI) * RL::kBlock + (g0 % VI) * (int)sizeof(TI);
@@ -344,13 +362,18 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
         // whole chunks: every lane stores (rows past the group end fall outside the
         // buffer range and are dropped), so the store count is static and the next
         // chunk's prefetch wait does not have to drain these stores
-        const uint32_t off = r < nrows ? (uint32_t)(r * a.o_ds + col0) * (uint32_t)sizeof(TI) : 0x80000000u;
-        buf_st16(rs_out, off, pack_f<TI>(o));
-      } else if (r < nrows) {
-        TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
+        const uint32_t off = r < nrows ? (uint32_t)(r * a.o_ds + (rev ? cm : col0)) * (uint32_t)sizeof(TI) : 0x80000000u;
         const uint4 ov = pack_f<TI>(o);
-        if (full) st16(dst, ov);
-        else st16_masked(dst, ov, nv);
+        buf_st16(rs_out, off, rev ? reverse_elems<TI>(ov) : ov);
+      } else if (r < nrows) {
+        const uint4 ov = pack_f<TI>(o);
+        if (rev) {
+          st16_rev(out + (int64_t)(dbase + r) * a.o_ds, cm, ov, nv);
+        } else {
+          TI* dst = out + (int64_t)(dbase + r) * a.o_ds + col0;
+          if (full) st16(dst, ov);
+          else st16_masked(dst, ov, nv);
+        }
       }
     }
     wave_lds_sync();  // next chunk's staging overwrites the rows
@@ -678,8 +701,19 @@ static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
             return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
     case 4: if (aligned && a.seqlen % kT == 0) return launch_fwd_v<TI, kN, 2, false, true, 3>(a, aligned, s);
             return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
-    default: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
+    default: return launch_fwd_v<TI, kN, 4, true, true, sizeof(TI) == 4 ? 1 : 2>(a, aligned, s);   // fp32: see launch_fwd_dirs
   }
+}
+
+template <typename TI>
+static int launch_fwd_dirs(const FwdArgs& a, bool aligned, hipStream_t s) {
+  // fp32 rows double the prefetch registers: one wave per SIMD keeps them out of scratch
+  // (the SS2D grids are a few hundred waves, occupancy buys nothing there)
+  constexpr int kW = sizeof(TI) == 4 ? 1 : 2;
+  const int np = padded_dstate(a.dstate);
+  if (np == 8) return launch_fwd_v<TI, 8, 4, true, true, kW>(a, aligned, s);
+  if (np == 16) return launch_fwd_v<TI, 16, 4, true, true, kW>(a, aligned, s);
+  return launch_fwd_v<TI, 32, 4, true, true, kW>(a, aligned, s);
 }
 
 template <typename TI>
@@ -741,9 +775,18 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   MC_CHECK(p->workspace && p->workspace_bytes >= need && aligned16(p->workspace), MC_ERR_WORKSPACE,
            "mc_scan_fwd: workspace must be >= %zu bytes and 16-B aligned (got %zu)", need, p->workspace_bytes);
 
+  const bool dirs = p->reverse_groups != 0 || p->u_groups != 0;
+  if (dirs) {
+    MC_CHECK(!p->z && p->u_groups >= 0 && p->u_groups <= p->n_groups && p->n_groups <= 31 &&
+                 (p->reverse_groups >> p->n_groups) == 0,
+             MC_ERR_SHAPE, "mc_scan_fwd: reverse_groups / u_groups need no z, 0 <= u_groups <= n_groups <= 31 and "
+             "a mask within n_groups (got mask 0x%x, u_groups %d, n_groups %d)", p->reverse_groups, p->u_groups,
+             p->n_groups);
+  }
   hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
                              p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
-                             p->seqlen, p->dstate, reinterpret_cast<float*>(p->workspace), s);
+                             p->seqlen, p->dstate, dirs ? p->reverse_groups : 0,
+                             reinterpret_cast<float*>(p->workspace), s);
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
 
   FwdArgs a;
@@ -762,6 +805,7 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   a.D = p->D; a.z = p->z; a.delta_bias = p->delta_bias;
   a.out = p->out; a.chunk_states = p->chunk_states; a.last_state = p->last_state;
   a.out_y = p->z ? p->out_y : nullptr; a.y_bs = p->out_y_batch_stride; a.y_ds = p->out_y_dim_stride;
+  a.rev_groups = dirs ? p->reverse_groups : 0; a.u_groups = dirs ? p->u_groups : 0;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
@@ -769,6 +813,12 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
                        vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
                        vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
+  if (dirs) {   // per-group addressing lives in the LDS-staged kernel (vector modes: seqlen % VI == 0)
+    const bool al = aligned && p->seqlen % (16 / ib) == 0;
+    if (p->itype == MC_DTYPE_F32) return launch_fwd_dirs<float>(a, al, s);
+    if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
+    return launch_fwd_dirs<f16_t>(a, al, s);
+  }
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
   return launch_fwd_t<f16_t>(a, aligned, s);

@@ -34,6 +34,7 @@ class ScanFwdParams(ctypes.Structure):
         ("out", c_vp), ("chunk_states", c_fp), ("last_state", c_fp),
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
         ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
+        ("reverse_groups", c_i32), ("u_groups", c_i32),
     ]
 
 
@@ -57,6 +58,7 @@ class ScanBwdParams(ctypes.Structure):
         ("dA", c_fp), ("dD", c_fp), ("ddelta_bias", c_fp),
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
         ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
+        ("reverse_groups", c_i32), ("u_groups", c_i32),
     ]
 
 

@@ -28,7 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .ops import add_layernorm, add_rmsnorm, causal_conv1d, linear_sk, patch_im2col, wleft_mm
-from .selective_scan_interface import selective_scan_fn
+from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, grouped_scan_fn,
+                                       selective_scan_fn)
 
 
 # ============================================================================ Mamba text tower
@@ -511,34 +512,43 @@ class SS2D(nn.Module):
         self.out_proj = nn.Linear(di, d_model, bias=bias)
         self.dropout = nn.Dropout(dropout) if dropout > 0.0 else None
 
-    def forward_core(self, x):  # (B, d, H, W) -> four (B, d, L) maps, fp32
+    def _scan_dirs(self, x):  # (B, d, H, W) -> (B, 4, d, L) outputs, directions in their own frames
+        """model.py:503-565 with the flips inside the scan kernel's addressing: u = [x, x^T] is the only
+        copy (the reference stacks [x, x^T, flip x, flip x^T]); the per-direction projections read it
+        in place; directions 2 / 3 walk u blocks 0 / 1 backwards (grouped_scan_fn), so their outputs
+        come back un-flipped.  Blocks 1 / 3 are still in the transposed (W, H) frame."""
         Bsz, d, H, W = x.shape
         L, K = H * W, 4
-        x_hw = x.reshape(Bsz, d, L)
-        x_wh = x.transpose(2, 3).reshape(Bsz, d, L)
-        xs = torch.stack([x_hw, x_wh, x_hw.flip(-1), x_wh.flip(-1)], dim=1)          # (B, K, d, L)
-        x_dbl = torch.einsum("bkdl,kcd->bkcl", xs, self.x_proj_weight.to(xs.dtype))
+        u = torch.stack([x.reshape(Bsz, d, L), x.transpose(2, 3).reshape(Bsz, d, L)], dim=1)   # (B, 2, d, L)
+        w = self.x_proj_weight.to(u.dtype).view(2, 2, -1, d)                # [i][j]: direction k = 2 i + j
+        x_dbl = torch.einsum("bjdl,ijcd->bijcl", u, w).reshape(Bsz, K, -1, L)
         dts, Bs, Cs = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=2)
-        dts = torch.einsum("bkrl,kdr->bkdl", dts, self.dt_projs_weight.to(xs.dtype))
-        out = selective_scan_fn(xs.float().reshape(Bsz, K * d, L), dts.float().reshape(Bsz, K * d, L),
-                                -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
-                                z=None, delta_bias=self.dt_projs_bias.float().reshape(-1), delta_softplus=True)
-        out = out.reshape(Bsz, K, d, L)
-        y_inv = out[:, 2:4].flip(-1)
-        y_wh = out[:, 1].reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, L)
-        y_invwh = y_inv[:, 1].reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, L)
-        return out[:, 0], y_inv[:, 0], y_wh, y_invwh
+        dts = torch.einsum("bkrl,kdr->bkdl", dts, self.dt_projs_weight.to(u.dtype))
+        out = grouped_scan_fn(u.float().reshape(Bsz, 2 * d, L), dts.float().reshape(Bsz, K * d, L),
+                              -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
+                              self.dt_projs_bias.float().reshape(-1), delta_softplus=True,
+                              reverse_groups=SS2D_REVERSE_GROUPS, u_groups=SS2D_U_GROUPS)
+        return out.view(Bsz, K, d, L)
+
+    def forward_core(self, x):  # (B, d, H, W) -> four (B, d, L) maps, fp32, reference order
+        Bsz, d, H, W = x.shape
+        out = self._scan_dirs(x)
+        back = lambda t: t.reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, H * W)  # noqa: E731
+        return out[:, 0], out[:, 2], back(out[:, 1]), back(out[:, 3])
 
     def forward(self, x, **kwargs):  # (B, H, W, C)
         Bsz, H, W, _ = x.shape
         x, z = self.in_proj(x).chunk(2, dim=-1)
         x = self.act(self.conv2d(x.permute(0, 3, 1, 2).contiguous()))
-        y1, y2, y3, y4 = self.forward_core(x)
-        y = (y1 + y2 + y3 + y4).transpose(1, 2).reshape(Bsz, H, W, -1)
+        out = self._scan_dirs(x)
+        d = out.shape[2]
+        # merge (model.py:553-565, 643): one transpose back for the two column-major directions
+        y_t = (out[:, 1] + out[:, 3]).view(Bsz, d, W, H)
+        y = (out[:, 0] + out[:, 2]).view(Bsz, d, H, W) + y_t.transpose(2, 3)
+        y = y.permute(0, 2, 3, 1)
         y = self.out_norm(y) * F.silu(z)
         out = self.out_proj(y)
         return self.dropout(out) if self.dropout is not None else out
-
 
 def channel_shuffle(x, groups):
     Bsz, H, W, C = x.shape

@@ -56,18 +56,23 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
         raise RuntimeError("selective_scan_fn: dim must be divisible by n_groups")
 
 
-def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False):
+def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False,
+             dirs=None):
     """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None[, out_y]).
+
+    ``dirs=(reverse_groups, u_groups)``: grouped directions (include/mc_scan.h):
+    mirrored positions for the reversed groups, u shared in u_groups blocks.
 
     ``want_y`` (with z): also return the pre-gate output y + D u -- upstream's
     forward returns it as ``out`` next to ``out_z``.  Training does not need it:
     the backward recomputes y from the chunk states.
     """
     lib = _lib.load()
-    batch, dim, L = u.shape
+    batch, dim, L = delta.shape
     dstate = A.shape[1]
     G = B.shape[1]
-    out = torch.empty_like(u)      # same (dense) layout as u: channel-major callers stay channel-major
+    # same (dense) layout as u: channel-major callers stay channel-major
+    out = torch.empty_like(u) if dirs is None else torch.empty_like(delta)
     nch = _lib.MC_SCAN_CHUNK and lib.mc_scan_n_chunks(L)
     states = (torch.empty(batch, dim, nch, dstate, device=u.device, dtype=torch.float32)
               if want_states else None)
@@ -90,6 +95,8 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     ws_bytes = lib.mc_scan_fwd_workspace_bytes(batch, L, dstate, G)
     ws = torch.empty(max(ws_bytes, 1), device=u.device, dtype=torch.uint8)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
+    if dirs is not None:
+        p.reverse_groups, p.u_groups = int(dirs[0]), int(dirs[1])
     out_y = torch.empty_like(u) if (want_y and z is not None) else None
     if out_y is not None:
         p.out_y, p.out_y_batch_stride, p.out_y_dim_stride = out_y.data_ptr(), out_y.stride(0), out_y.stride(1)
@@ -101,13 +108,15 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None):
+    """Run mc_scan_bwd.  With ``dirs``, du comes back per group, (B, dim, L): the caller sums the
+    groups that share a u block."""
     lib = _lib.load()
-    batch, dim, L = u.shape
+    batch, dim, L = delta.shape
     dstate = A.shape[1]
     G = B.shape[1]
     dout = _last_dim_contig(dout)
-    du = torch.empty_like(u)
+    du = torch.empty_like(u) if dirs is None else torch.empty_like(delta)
     ddelta = torch.empty_like(delta)
     dz = torch.empty_like(z) if z is not None else None
     dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
@@ -138,6 +147,8 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states):
     p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
     p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
+    if dirs is not None:
+        p.reverse_groups, p.u_groups = int(dirs[0]), int(dirs[1])
     _lib.check(lib.mc_scan_bwd(p, _lib.stream_handle(u.device)), "mc_scan_bwd")
     return du, ddelta, dA, dB, dC, dD, dz, dbias
 
@@ -193,3 +204,63 @@ def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_
     last position.  Output dtype = u.dtype.
     """
     return SelectiveScanFn.apply(u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state)
+
+
+class GroupedScanFn(torch.autograd.Function):
+    """Scan whose n_groups groups are independent directions: group g reads u block
+    g % u_groups and, if bit g of reverse_groups is set, walks its sequence backwards
+    at mirrored positions (mc_scan_*_params.reverse_groups / u_groups).  SS2D's four
+    cross-scan directions are ONE call per pass on u = [x, x^T]: no flipped copies
+    of the inputs, no un-flip of the outputs (reference model.py:510-517, 553-565)."""
+
+    @staticmethod
+    def forward(ctx, u, delta, A, B, C, D, delta_bias, delta_softplus, reverse_groups, u_groups):
+        u, delta = _last_dim_contig(u), _last_dim_contig(delta)
+        B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
+        A32 = A.float().contiguous()
+        D32 = D.float().contiguous() if D is not None else None
+        bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
+        batch, dim, L = delta.shape
+        G = B.shape[1]
+        if (dim % G or u.shape != (batch, u_groups * (dim // G), L) or B.shape[0] != batch
+                or B.shape[3] != L or C.shape != B.shape):
+            raise RuntimeError("grouped_scan_fn: u (B, u_groups*dim/G, L), delta (B, dim, L), B/C (B, G, N, L) expected")
+        if not u.is_cuda or delta.dtype != u.dtype or C.dtype != B.dtype:
+            raise RuntimeError("grouped_scan_fn: GPU tensors; u / delta and B / C must share dtypes")
+        need_grad = any(ctx.needs_input_grad[:7])
+        dirs = (int(reverse_groups), int(u_groups))
+        out, states, _ = scan_fwd(u, delta, A32, B, C, D32, None, bias32, delta_softplus, want_states=need_grad,
+                                  want_last=False, dirs=dirs)
+        if need_grad:
+            ctx.save_for_backward(u, delta, A32, B, C, D32, bias32, states)
+        ctx.cfg = (delta_softplus, dirs, A.dtype, D.dtype if D is not None else None,
+                   delta_bias.dtype if delta_bias is not None else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, delta, A32, B, C, D32, bias32, states = ctx.saved_tensors
+        softplus, dirs, a_dt, d_dt, b_dt = ctx.cfg
+        du, ddelta, dA, dB, dC, dD, _, dbias = scan_bwd(u, delta, A32, B, C, D32, None, bias32, softplus, dout,
+                                                        states, dirs=dirs)
+        G, k = B.shape[1], dirs[1]
+        # u block j's gradient: sum of the groups g = j (mod k) that read it (fp32 accumulate;
+        # with 16-bit I/O each group's part was rounded once to the I/O dtype by the kernel)
+        batch, dim, L = du.shape
+        du_u = du.view(batch, G // k, k, dim // G, L).sum(1, dtype=torch.float32).to(u.dtype).view(u.shape)
+        return (du_u, ddelta, dA.to(a_dt), dB, dC, dD.to(d_dt) if dD is not None else None,
+                dbias.to(b_dt) if dbias is not None else None, None, None, None)
+
+
+def grouped_scan_fn(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=False, reverse_groups=0,
+                    u_groups=1):
+    """out (B, dim, L) = selective scan of each of the n_groups = B.shape[1] groups, where group g
+    reads u block g % u_groups (u: (B, u_groups * dim / n_groups, L)) and runs backwards over
+    mirrored positions if bit g of reverse_groups is set (its output lands at the positions it
+    read).  delta (B, dim, L); B, C (B, n_groups, N, L); A (dim, N); D, delta_bias (dim,)."""
+    return GroupedScanFn.apply(u, delta, A, B, C, D, delta_bias, delta_softplus, reverse_groups, u_groups)
+
+
+# SS2D's four cross-scan directions over u = [x, x^T]: 0 = x, 1 = x^T, 2 = flip(x), 3 = flip(x^T)
+SS2D_REVERSE_GROUPS = 0b1100
+SS2D_U_GROUPS = 2

@@ -41,7 +41,28 @@ def _im2col(img, P):
     return F.unfold(img, P, stride=P).transpose(1, 2).reshape(B * (H // P) * (W // P), C * P * P)
 
 
-_OPS = {"selective_scan_fn": selective_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
+def grouped_scan_ref(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=False, reverse_groups=0,
+                     u_groups=1):
+    """Restatement of the grouped-direction scan with EXPLICIT copies, the way the reference builds
+    SS2D's cross-scan (model.py:510-517: stack, flip) and merges it (553-565: flip back): group g
+    scans u block g % u_groups, flipped along L when bit g of reverse_groups is set, and its output
+    is flipped back."""
+    Bsz, dim, L = delta.shape
+    G = B.shape[1]
+    d = dim // G
+    ub = u.view(Bsz, u_groups, d, L)
+    rev = [bool((reverse_groups >> g) & 1) for g in range(G)]
+    fl = lambda t, g: t.flip(-1) if rev[g] else t  # noqa: E731
+    xs = torch.stack([fl(ub[:, g % u_groups], g) for g in range(G)], 1).reshape(Bsz, dim, L)
+    dl = torch.stack([fl(delta.view(Bsz, G, d, L)[:, g], g) for g in range(G)], 1).reshape(Bsz, dim, L)
+    Bs = torch.stack([fl(B[:, g], g) for g in range(G)], 1)
+    Cs = torch.stack([fl(C[:, g], g) for g in range(G)], 1)
+    out = selective_scan_ref(xs, dl, A, Bs, Cs, D, delta_bias=delta_bias, delta_softplus=delta_softplus)
+    out = out.view(Bsz, G, d, L)
+    return torch.stack([fl(out[:, g], g) for g in range(G)], 1).reshape(Bsz, dim, L)
+
+
+_OPS = {"selective_scan_fn": selective_scan_ref, "grouped_scan_fn": grouped_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
         "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col, "add_layernorm": _add_layernorm_f32}
 
 

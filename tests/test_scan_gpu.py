@@ -251,3 +251,57 @@ def test_scan_bwd_deterministic():
         grads.append({k: v.grad.clone() for k, v in leaves.items()})
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+# ----------------------------------------------------------------- grouped directions (SS2D cross-scan)
+@pytest.mark.parametrize("Bsz,d,L,rev,ug,dt", [(2, 64, 35, 0b1100, 2, torch.float32),
+                                               (1, 96, 256, 0b1100, 2, torch.float32),
+                                               (2, 40, 36, 0b1010, 1, torch.bfloat16),
+                                               (1, 128, 784, 0b0110, 4, torch.float32),
+                                               (2, 64, 49, 0b1111, 2, torch.float16)])
+def test_grouped_scan_matches_explicit_flips(Bsz, d, L, rev, ug, dt):
+    """Mirrored addressing of reversed groups and shared u blocks inside the kernels vs the
+    reference's explicit stack / flip / flip-back around a plain scan (oracle.cpu_model.grouped_scan_ref,
+    fp64 autograd): outputs and every gradient.  L = 35 / 49 leave the mirrored 16-B blocks unaligned."""
+    from mamba_clip_amd.selective_scan_interface import grouped_scan_fn
+    from oracle.cpu_model import grouped_scan_ref
+    N, G = 16, 4
+    g = torch.Generator().manual_seed(L * 10 + d)
+    u = torch.randn(Bsz, ug * d, L, generator=g).to(dt)
+    delta = (0.5 * torch.randn(Bsz, G * d, L, generator=g)).to(dt)
+    A = -torch.exp(torch.log(torch.arange(1, N + 1, dtype=torch.float32)).repeat(G * d, 1)
+                   + 0.1 * torch.randn(G * d, N, generator=g))
+    Bm = torch.randn(Bsz, G, N, L, generator=g)
+    Cm = torch.randn(Bsz, G, N, L, generator=g)
+    Dv = torch.randn(G * d, generator=g)
+    bias = torch.rand(G * d, generator=g) * 4 - 5
+    dout = torch.randn(Bsz, G * d, L, generator=g)
+    ins = dict(u=u, delta=delta, A=A, B=Bm, C=Cm, D=Dv, delta_bias=bias)
+    ref_in = {k: v.double().requires_grad_(True) for k, v in ins.items()}
+    ref = grouped_scan_ref(**ref_in, delta_softplus=True, reverse_groups=rev, u_groups=ug)
+    ref.backward(dout.to(dt).double())
+    dev_in = {k: v.to(DEV).requires_grad_(True) for k, v in ins.items()}
+    out = grouped_scan_fn(**dev_in, delta_softplus=True, reverse_groups=rev, u_groups=ug)
+    assert out.shape == (Bsz, G * d, L) and out.dtype == dt
+    assert_scan_close(out, ref.detach(), dt)
+    out.backward(dout.to(DEV).to(dt))
+    for k in ins:
+        if k == "u" and dt != torch.float32 and ug < G:
+            # du of a shared block = sum of G / ug groups' parts, each rounded once to the I/O dtype
+            err = (dev_in[k].grad.float().cpu() - ref_in[k].grad.float()).abs()
+            lim = (G // ug) * GRAD_REL[dt] * float(ref_in[k].grad.abs().max())
+            assert float(err.max()) <= lim, (float(err.max()), lim)
+            continue
+        assert_grad_close(dev_in[k].grad, ref_in[k].grad, dev_in[k].dtype, k)
+
+
+def test_grouped_scan_rejects_bad_configs():
+    from mamba_clip_amd.selective_scan_interface import grouped_scan_fn
+    A = -torch.ones(32, 16, device=DEV)
+    Bm = torch.randn(1, 4, 16, 12, device=DEV)
+    with pytest.raises(RuntimeError):   # u has the wrong number of shared blocks
+        grouped_scan_fn(torch.randn(1, 24, 12, device=DEV), torch.randn(1, 32, 12, device=DEV), A, Bm, Bm,
+                        reverse_groups=0b1100, u_groups=2)
+    with pytest.raises(RuntimeError):   # mask beyond n_groups
+        grouped_scan_fn(torch.randn(1, 16, 12, device=DEV), torch.randn(1, 32, 12, device=DEV), A, Bm, Bm,
+                        reverse_groups=0b110000, u_groups=2)
