@@ -53,10 +53,12 @@ int mc_add_layernorm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* 
                          const float* bias, float eps, void* y, void* h_out, float* mean, float* rstd, void* stream);
 
 /* Backward of (y, h) = add_layernorm(x, res): dx = dres = dh + d(LN)/dh . dy  (dh nullable),
- * dw, dbias (cols,) fp32 (dbias nullable); deterministic reductions in workspace. */
+ * dw, dbias (cols,) fp32 (dbias nullable); dx_colsum (cols,) fp32, nullable: the column
+ * sums of dx as stored -- the bias gradient of the linear layer that produced x (ViT/BERT
+ * fc2 and attention proj), taken in this pass.  Deterministic reductions in workspace. */
 int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const void* dh, const void* h,
                          const float* w, const float* mean, const float* rstd, void* dx, float* dw, float* dbias,
-                         void* workspace, size_t workspace_bytes, void* stream);
+                         float* dx_colsum, void* workspace, size_t workspace_bytes, void* stream);
 size_t mc_add_layernorm_bwd_workspace_bytes(int32_t rows, int32_t cols);
 
 /* y[b, d, t] = act( bias[d] + sum_k w[d, k] * x[b, d, t - (K-1) + k] ), zero left padding.
@@ -78,6 +80,35 @@ size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t 
  * img (batch, C, H, W) contiguous; H % P == W % P == 0; same dtype in and out. */
 int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, int32_t P, int32_t dtype, const void* img,
                     void* patches, void* stream);
+
+/* Fused gradient passes that also produce the bias gradient of the GEMM in
+ * front of them, in the same single stream over the (rows x cols) gradient
+ * (rows 16-B aligned, cols a multiple of 8 / 4 for 16-bit / fp32):
+ * mc_gelu_bwd: gh = ga * gelu'(h)  (exact erf GELU, torch approximate='none'),
+ *              dbias[c] = sum_rows gh[:, c]  -- the ViT / BERT MLP's fc1 bias;
+ * mc_qkv_grad_pack: the attention's q / k / v gradients (three (batch, seq,
+ *              heads, head_dim) tensors, any batch / token / head strides,
+ *              head_dim contiguous) packed into the qkv projection's output
+ *              gradient (batch*seq, 3*heads*head_dim) -- the layout of its
+ *              (B, N, 3, H, D) view -- plus its column sums (the qkv bias, nullable).
+ * Column sums are fp32, of the stored (rounded) values, deterministic
+ * (fixed-order slice partials in the workspace, mc_grad_colsum_workspace_bytes).
+ * Replace the unfused torch sequence GELU-backward + sum(0) and
+ * stack(dq, dk, dv) + sum(0) behind the towers' MLP / attention (timm Block,
+ * open_clip VisionTransformer as loaded at reference model.py:1270). */
+size_t mc_grad_colsum_workspace_bytes(int32_t rows, int32_t cols);
+int mc_gelu_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* h, int64_t ldh, const void* ga, int64_t ldga,
+                void* gh, int64_t ldgh, float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+
+typedef struct mc_qkv_pack_params {
+  int32_t batch, seq, heads, head_dim, dtype;
+  const void* src[3];                 /* dq, dk, dv */
+  int64_t sb[3], sn[3], sh[3];        /* element strides of batch, token, head per source */
+  void* out; int64_t ld_out;
+  float* dbias;                       /* nullable */
+  void* workspace; size_t workspace_bytes;
+} mc_qkv_pack_params;
+int mc_qkv_grad_pack(const mc_qkv_pack_params* p, void* stream);
 
 #ifdef __cplusplus
 }

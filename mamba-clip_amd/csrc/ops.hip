@@ -179,21 +179,24 @@ __global__ __launch_bounds__(256) void colsum_pass1_kernel(const float* __restri
 }
 
 __global__ __launch_bounds__(256) void colsum_pass2_kernel(const float* __restrict__ tmp, int cols, int split,
-                                                           float* __restrict__ out0, float* __restrict__ out1) {
+                                                           float* __restrict__ out0, float* __restrict__ out1,
+                                                           float* __restrict__ out2) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   float s = 0.f;
 #pragma unroll 8
   for (int k = 0; k < kColSlices; ++k) s += tmp[(int64_t)k * cols + c];
   if (c < split) out0[c] = s;
-  else if (out1) out1[c - split] = s;
+  else if (c < 2 * split) { if (out1) out1[c - split] = s; }
+  else if (out2) out2[c - 2 * split] = s;
 }
 
+// columns [0, split) -> out0, [split, 2 split) -> out1, [2 split, cols) -> out2 (out1 / out2 nullable)
 static void colsum_two_pass(const float* in, int nrows, int cols, int split, float* out0, float* out1, float* tmp,
-                            hipStream_t s) {
+                            hipStream_t s, float* out2 = nullptr) {
   const int gx = (cols + 255) / 256;
   hipLaunchKernelGGL(colsum_pass1_kernel, dim3(gx, kColSlices), dim3(256), 0, s, in, nrows, cols, tmp);
-  hipLaunchKernelGGL(colsum_pass2_kernel, dim3(gx), dim3(256), 0, s, tmp, cols, split, out0, out1);
+  hipLaunchKernelGGL(colsum_pass2_kernel, dim3(gx), dim3(256), 0, s, tmp, cols, split, out0, out1, out2);
 }
 
 constexpr int kNormGrid = 512;  // blocks of 4 waves: 2048 waves -> 2048 dw partial rows
@@ -281,8 +284,10 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
 }
 
 // dh_total = dh + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
-// dx (= dres) = dh_total;  part rows: [wave][0..cols) dw, [wave][cols..2cols) db
-template <typename T, int NV>
+// dx (= dres) = dh_total;  part rows: [wave][0..cols) dw, [wave][cols..2cols) db and, with kDxSum,
+// [wave][2cols..3cols) the column sums of dx as stored: the bias gradient of the layer whose output
+// entered as x (fc2 / attention proj), taken in this pass instead of a second read of dx
+template <typename T, int NV, bool kDxSum>
 __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                                 const T* __restrict__ dh,
                                                                 const T* __restrict__ hbuf,
@@ -295,12 +300,12 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int nvec = cols / V;
-  float wr[NV][V], dwacc[NV][V], dbacc[NV][V];
+  float wr[NV][V], dwacc[NV][V], dbacc[NV][V], dxacc[kDxSum ? NV : 1][V];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int v = lane + 64 * i;
 #pragma unroll
-    for (int e = 0; e < V; ++e) { dwacc[i][e] = 0.f; dbacc[i][e] = 0.f; }
+    for (int e = 0; e < V; ++e) { dwacc[i][e] = 0.f; dbacc[i][e] = 0.f; if constexpr (kDxSum) dxacc[i][e] = 0.f; }
     if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
   }
   for (int row = wave; row < rows; row += nwaves) {
@@ -345,16 +350,23 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
           o[e] = rs * (g[i][e] - mg - xh[i][e] * mgx);
           if (dh) o[e] += elem_f<T>(dq, e);
         }
-        st16(dx + off, pack_f<T>(o));
+        const uint4 oq = pack_f<T>(o);
+        st16(dx + off, oq);
+        if constexpr (kDxSum) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) dxacc[i][e] += elem_f<T>(oq, e);
+        }
       }
     }
   }
+  constexpr int kW = kDxSum ? 3 : 2;   // partial columns per wave
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int v = lane + 64 * i;
     if (v < nvec) {
-      st_f32v<V>(part + (int64_t)wave * 2 * cols + v * V, dwacc[i]);
-      st_f32v<V>(part + (int64_t)wave * 2 * cols + cols + v * V, dbacc[i]);
+      st_f32v<V>(part + (int64_t)wave * kW * cols + v * V, dwacc[i]);
+      st_f32v<V>(part + (int64_t)wave * kW * cols + cols + v * V, dbacc[i]);
+      if constexpr (kDxSum) st_f32v<V>(part + (int64_t)wave * kW * cols + 2 * cols + v * V, dxacc[i]);
     }
   }
 }
@@ -419,12 +431,15 @@ __device__ __forceinline__ void load_window(const T* __restrict__ xr, int t0, in
   }
 }
 
-template <typename T, int VEC>
-__global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+// KC: the tap count as a compile-time constant (4: Mamba's d_conv) or 0 = runtime K <= kMaxK.
+template <typename T, int VEC, int KC>
+__global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K_, const T* __restrict__ x,
                                                          int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int silu,
                                                          T* __restrict__ y, int64_t y_bs, int64_t y_ds) {
-  constexpr int NP = (kMaxK - 1 + VEC - 1) / VEC;   // previous vectors covering the K-1 halo
+  constexpr int KM = KC ? KC : kMaxK;
+  const int K = KC ? KC : K_;
+  constexpr int NP = (KM - 1 + VEC - 1) / VEC;   // previous vectors covering the K-1 halo
   const int nchunk = (L + VEC - 1) / VEC;
   const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= (int64_t)batch * dim * nchunk) return;
@@ -434,16 +449,16 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int
   const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
   float win[(NP + 1) * VEC];
   load_window<T, VEC, NP, 0>(xr, t0, L, win);
-  float wk[kMaxK];
+  float wk[KM];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
+  for (int k = 0; k < KM; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
   const float bv = bias ? bias[d] : 0.f;
   float out[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     float acc = bv;
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k)   // tap k reads position t0 + i - (K-1) + k
+    for (int k = 0; k < KM; ++k)   // tap k reads position t0 + i - (K-1) + k
       if (k < K) acc = fmaf(wk[k], win[NP * VEC + i - (K - 1) + k], acc);
     out[i] = silu ? silu_f(acc) : acc;
   }
@@ -455,17 +470,19 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int
 // forms g = dy * act'(pre), writes dx for its VEC positions and accumulates
 // dw / dbias in registers; a wave reduction then writes one partial per
 // (slice, d) -- deterministic, no atomics.
-template <typename T, int VEC>
-__global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int L, int K, const T* __restrict__ x,
+template <typename T, int VEC, int KC>
+__global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int L, int K_, const T* __restrict__ x,
                                                          int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int silu,
                                                          const T* __restrict__ dy, int64_t dy_bs, int64_t dy_ds,
                                                          T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
                                                          int items_per_slice, float* __restrict__ part) {
-  constexpr int NP = (kMaxK - 1 + VEC - 1) / VEC;
+  constexpr int KM = KC ? KC : kMaxK;
+  const int K = KC ? KC : K_;
+  constexpr int NP = (KM - 1 + VEC - 1) / VEC;
   constexpr int NN = NP;                             // following vectors covering t0+VEC .. t0+VEC+K-2
   constexpr int W = (NP + 1 + NN) * VEC;
-  constexpr int G = VEC + kMaxK - 1;                 // g positions t0 .. t0+VEC+K-2
+  constexpr int G = VEC + KM - 1;                    // g positions t0 .. t0+VEC+K-2
   const int lane = threadIdx.x & 63;
   const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (d >= dim) return;
@@ -474,13 +491,13 @@ __global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int
   const int total = batch * nchunk;
   const int i_begin = slice * items_per_slice;
   const int i_end = min(total, i_begin + items_per_slice);
-  float wk[kMaxK];
+  float wk[KM];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
+  for (int k = 0; k < KM; ++k) wk[k] = k < K ? w[d * K + k] : 0.f;
   const float bv = bias ? bias[d] : 0.f;
-  float dwk[kMaxK], db = 0.f;
+  float dwk[KM], db = 0.f;
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) dwk[k] = 0.f;
+  for (int k = 0; k < KM; ++k) dwk[k] = 0.f;
   for (int item = i_begin + lane; item < i_end; item += 64) {
     const int b = item / nchunk;
     const int t0 = (item - b * nchunk) * VEC;
@@ -508,7 +525,7 @@ __global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int
     for (int j = 0; j < G; ++j) {
       float pre = bv;
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k)
+      for (int k = 0; k < KM; ++k)
         if (k < K) pre = fmaf(wk[k], win[NP * VEC + j - (K - 1) + k], pre);
       float gj = gy[j];                               // zero beyond L (loaded as 0)
       if (silu) {
@@ -522,12 +539,12 @@ __global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int
     for (int i = 0; i < VEC; ++i) {
       float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k)               // dx[t] = sum_k w[k] g[t + K-1-k]
+      for (int k = 0; k < KM; ++k)                  // dx[t] = sum_k w[k] g[t + K-1-k]
         if (k < K) acc = fmaf(wk[k], g[i + (K - 1) - k], acc);
       out[i] = acc;
       db += g[i];
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k)
+      for (int k = 0; k < KM; ++k)
         if (k < K) dwk[k] = fmaf(g[i], win[NP * VEC + i - (K - 1) + k], dwk[k]);
     }
     store_vec<T, VEC>(dxr + t0, out);
@@ -535,13 +552,13 @@ __global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k) dwk[k] += __shfl_xor(dwk[k], o);
+    for (int k = 0; k < KM; ++k) dwk[k] += __shfl_xor(dwk[k], o);
     db += __shfl_xor(db, o);
   }
   if (lane == 0) {
     float* pr = part + ((int64_t)slice * dim + d) * (kMaxK + 1);
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k) pr[k] = dwk[k];
+    for (int k = 0; k < KM; ++k) pr[k] = dwk[k];   // slots >= K are never read
     pr[kMaxK] = db;
   }
 }
@@ -586,6 +603,145 @@ __global__ __launch_bounds__(256) void im2col_kernel(int batch, int C, int H, in
 }
 
 }  // namespace ops
+// ------------------------------------------------------------------ fused bias-gradient passes
+// Both kernels stream a (rows x cols) gradient once, coalesced along the row
+// (a wave = 64 consecutive 16-B column vectors of one row), write it, and sum
+// its columns on the way -- the bias gradient the unfused path gets from a
+// second full read.  Block = 64 column vectors x 4 row lanes over one row
+// slice; the 4 lanes meet in LDS and one fp32 partial per (slice, column)
+// goes to the workspace; colsum_slices_kernel folds the slices in order
+// (deterministic, no atomics).  The sums are of the values as stored (rounded
+// to the activation dtype), like the unfused reduction.
+constexpr int kGradSlices = 512;
+
+__device__ __forceinline__ float gelu_grad_f(float x) {   // d/dx [x * Phi(x)], exact erf form (torch 'none')
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return fmaf(x, pdf, cdf);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(int rows, int cols, const T* __restrict__ h, int64_t ldh,
+                                                              const T* __restrict__ ga, int64_t ldga, T* __restrict__ gh,
+                                                              int64_t ldgh, float* __restrict__ part) {
+  constexpr int V = ElemTraits<T>::kVec;
+  __shared__ float red[3][64 * V];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cv = blockIdx.x * 64 + lane;
+  const bool ok = cv < cols / V;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (ok) {
+    // two rows per step: both rows' loads are in flight before the first use
+    for (int r = r0 + rl; r < r1; r += 8) {
+      const int r2 = min(r + 4, r1 - 1);
+      const bool two = r + 4 < r1;
+      const uint4 hq = ld16(h + (int64_t)r * ldh + cv * V);
+      const uint4 gq = ld16(ga + (int64_t)r * ldga + cv * V);
+      const uint4 hq2 = ld16(h + (int64_t)r2 * ldh + cv * V);
+      const uint4 gq2 = ld16(ga + (int64_t)r2 * ldga + cv * V);
+      float o[V], o2[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        o[e] = elem_f<T>(gq, e) * gelu_grad_f(elem_f<T>(hq, e));
+        o2[e] = elem_f<T>(gq2, e) * gelu_grad_f(elem_f<T>(hq2, e));
+      }
+      const uint4 oq = pack_f<T>(o), oq2 = pack_f<T>(o2);
+      st16(gh + (int64_t)r * ldgh + cv * V, oq);
+      if (two) st16(gh + (int64_t)r2 * ldgh + cv * V, oq2);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += elem_f<T>(oq, e) + (two ? elem_f<T>(oq2, e) : 0.f);
+    }
+  }
+  if (rl > 0) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[rl - 1][lane * V + e] = acc[e];
+  }
+  __syncthreads();
+  if (rl == 0 && ok) {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      part[(int64_t)blockIdx.y * cols + cv * V + e] = ((acc[e] + red[0][lane * V + e]) + red[1][lane * V + e]) +
+                                                      red[2][lane * V + e];
+  }
+}
+
+// Attention q/k/v gradients -> the packed (B*N, 3*H*D) gradient of the qkv
+// projection output (the layout of its (B, N, 3, H, D) view) + its column sums.
+struct QkvSrc {
+  const void* p[3];
+  int64_t sb[3], sn[3], sh[3];   // element strides of (batch, token, head); head_dim stride 1
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void qkv_pack_colsum_kernel(int batch, int seq, int heads, int hd, const QkvSrc src,
+                                                              T* __restrict__ out, int64_t ldo, float* __restrict__ part) {
+  constexpr int V = ElemTraits<T>::kVec;
+  __shared__ float red[3][64 * V];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cols = 3 * heads * hd;
+  const int cv = blockIdx.x * 64 + lane;
+  const bool ok = cv < cols / V;
+  const int vph = hd / V;                         // vectors per head
+  const int s3 = ok ? cv / (heads * vph) : 0;
+  const int hh = ok ? (cv / vph) % heads : 0;
+  const int dv = ok ? cv % vph : 0;
+  const T* base = reinterpret_cast<const T*>(s3 == 0 ? src.p[0] : (s3 == 1 ? src.p[1] : src.p[2]));
+  const int64_t sb = s3 == 0 ? src.sb[0] : (s3 == 1 ? src.sb[1] : src.sb[2]);
+  const int64_t sn = s3 == 0 ? src.sn[0] : (s3 == 1 ? src.sn[1] : src.sn[2]);
+  const int64_t sh = s3 == 0 ? src.sh[0] : (s3 == 1 ? src.sh[1] : src.sh[2]);
+  base += (int64_t)hh * sh + dv * V;
+  const int rows = batch * seq;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (ok) {
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const int b = r / seq, n = r - b * seq;
+      const uint4 q = ld16(base + (int64_t)b * sb + (int64_t)n * sn);
+      st16(out + (int64_t)r * ldo + cv * V, q);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += elem_f<T>(q, e);
+    }
+  }
+  if (rl > 0) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[rl - 1][lane * V + e] = acc[e];
+  }
+  __syncthreads();
+  if (rl == 0 && ok && part) {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      part[(int64_t)blockIdx.y * cols + cv * V + e] = ((acc[e] + red[0][lane * V + e]) + red[1][lane * V + e]) +
+                                                      red[2][lane * V + e];
+  }
+}
+
+// out[c] = sum_k part[k][c]: a block = 32 columns x 8 slice lanes (independent loads in flight),
+// the 8 lane sums meet in LDS in a fixed order
+__global__ __launch_bounds__(256) void colsum_slices_kernel(const float* __restrict__ part, int nslices, int cols,
+                                                            float* __restrict__ out) {
+  __shared__ float red[8][33];
+  const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  float s = 0.f;
+  if (c < cols)
+    for (int k = q; k < nslices; k += 8) s += part[(int64_t)k * cols + c];
+  red[q][cx] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cx];
+    out[c] = t;
+  }
+}
+
 }  // namespace mc
 
 using namespace mc;
@@ -662,12 +818,13 @@ extern "C" int mc_add_layernorm_fwd(int32_t rows, int32_t cols, int32_t dtype, c
 
 extern "C" size_t mc_add_layernorm_bwd_workspace_bytes(int32_t rows, int32_t cols) {
   (void)rows;
-  return ((size_t)kNormGrid * 4 + kColSlices) * 2 * cols * sizeof(float);   // per-wave dw|db partials + slices
+  return ((size_t)kNormGrid * 4 + kColSlices) * 3 * cols * sizeof(float);   // per-wave dw|db|dxsum partials + slices
 }
 
 extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* dy, const void* dh,
                                     const void* h, const float* w, const float* mean, const float* rstd, void* dx,
-                                    float* dw, float* dbias, void* workspace, size_t workspace_bytes, void* stream) {
+                                    float* dw, float* dbias, float* dx_colsum, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
   MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_add_layernorm_bwd: bad dtype");
   const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
   MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0 && cols / V <= 64 * kMaxVec, MC_ERR_SHAPE,
@@ -678,11 +835,18 @@ extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, c
            "mc_add_layernorm_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   float* part = reinterpret_cast<float*>(workspace);
-  MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_bwd_kernel<T, NV>),
-      dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
-      part)));
-  // part is [wave][2 * cols]: dw in columns [0, cols), dbias in [cols, 2 cols)
-  colsum_two_pass(part, kNormGrid * 4, 2 * cols, cols, dw, dbias, part + (size_t)kNormGrid * 4 * 2 * cols, s);
+  const int kw = dx_colsum ? 3 : 2;
+  if (dx_colsum)
+    MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_bwd_kernel<T, NV, true>),
+        dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
+        part)));
+  else
+    MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_bwd_kernel<T, NV, false>),
+        dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
+        part)));
+  // part is [wave][kw * cols]: dw in columns [0, cols), dbias in [cols, 2 cols), dx sums in [2 cols, 3 cols)
+  colsum_two_pass(part, kNormGrid * 4, kw * cols, cols, dw, dbias, part + (size_t)kNormGrid * 4 * kw * cols, s,
+                  dx_colsum);
   return check_launch("mc_add_layernorm_bwd");
 }
 
@@ -711,8 +875,12 @@ extern "C" int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, 
   const int64_t items = (int64_t)batch * dim * ((seqlen + vec - 1) / vec);
   const dim3 grid((unsigned)((items + 255) / 256));
   MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
-    hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen, K,
-                       (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
+    if (K == 4)
+      hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC, 4>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen,
+                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
+    else
+      hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC, 0>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen,
+                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
   }));
   return check_launch("mc_causal_conv1d_fwd");
 }
@@ -750,12 +918,80 @@ extern "C" int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, 
   const int nslice = (total + per - 1) / per;
   const dim3 grid((unsigned)((dim + 3) / 4), (unsigned)nslice);
   MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
-    hipLaunchKernelGGL((conv1d_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, batch, dim, seqlen, K, (const T*)x, x_bs,
-                       x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
+    if (K == 4)   // Mamba's d_conv: taps unrolled at compile time
+      hipLaunchKernelGGL((conv1d_bwd_kernel<T, VEC, 4>), grid, dim3(256), 0, s, batch, dim, seqlen, K, (const T*)x,
+                         x_bs, x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
+    else
+      hipLaunchKernelGGL((conv1d_bwd_kernel<T, VEC, 0>), grid, dim3(256), 0, s, batch, dim, seqlen, K, (const T*)x,
+                         x_bs, x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
   }));
   const int n = dim * (K + 1);
   hipLaunchKernelGGL(conv1d_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, nslice, dim, K, dw, dbias);
   return check_launch("mc_causal_conv1d_bwd");
+}
+
+extern "C" size_t mc_grad_colsum_workspace_bytes(int32_t rows, int32_t cols) {
+  (void)rows;
+  return (size_t)kGradSlices * (size_t)std::max(cols, 0) * sizeof(float);
+}
+
+static int grad_slices(int rows) { return std::max(1, std::min(kGradSlices, (rows + 31) / 32)); }
+
+extern "C" int mc_gelu_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* h, int64_t ldh, const void* ga,
+                           int64_t ldga, void* gh, int64_t ldgh, float* dbias, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_gelu_bwd: bad dtype");
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(rows >= 0 && cols > 0 && cols % V == 0, MC_ERR_SHAPE, "mc_gelu_bwd: cols must be a multiple of %d", V);
+  if (rows == 0) {
+    if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)cols * 4, (hipStream_t)stream);
+    return MC_OK;
+  }
+  MC_CHECK(h && ga && gh && dbias, MC_ERR_INVALID, "mc_gelu_bwd: h, ga, gh, dbias required");
+  MC_CHECK(aligned16(h) && aligned16(ga) && aligned16(gh) && ldh % V == 0 && ldga % V == 0 && ldgh % V == 0,
+           MC_ERR_SHAPE, "mc_gelu_bwd: rows must be 16-B aligned");
+  MC_CHECK(workspace && workspace_bytes >= mc_grad_colsum_workspace_bytes(rows, cols), MC_ERR_WORKSPACE,
+           "mc_gelu_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(workspace);
+  const int ns = grad_slices(rows);
+  const dim3 grid((unsigned)((cols / V + 63) / 64), (unsigned)ns);
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((gelu_bwd_colsum_kernel<T>), grid, dim3(256), 0, s, rows, cols,
+                                          (const T*)h, ldh, (const T*)ga, ldga, (T*)gh, ldgh, part));
+  hipLaunchKernelGGL(colsum_slices_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, ns, cols, dbias);
+  return check_launch("mc_gelu_bwd");
+}
+
+extern "C" int mc_qkv_grad_pack(const mc_qkv_pack_params* p, void* stream) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_qkv_grad_pack: null params");
+  MC_CHECK(p->dtype >= MC_DTYPE_F32 && p->dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_qkv_grad_pack: bad dtype");
+  const int V = p->dtype == MC_DTYPE_F32 ? 4 : 8;
+  MC_CHECK(p->batch >= 0 && p->seq >= 0 && p->heads > 0 && p->head_dim > 0 && p->head_dim % V == 0, MC_ERR_SHAPE,
+           "mc_qkv_grad_pack: head_dim must be a multiple of %d", V);
+  const int rows = p->batch * p->seq, cols = 3 * p->heads * p->head_dim;
+  if (rows == 0) {
+    if (p->dbias) (void)hipMemsetAsync(p->dbias, 0, (size_t)cols * 4, (hipStream_t)stream);
+    return MC_OK;
+  }
+  QkvSrc src;
+  for (int i = 0; i < 3; ++i) {
+    MC_CHECK(p->src[i] && aligned16(p->src[i]) && p->sb[i] % V == 0 && p->sn[i] % V == 0 && p->sh[i] % V == 0,
+             MC_ERR_SHAPE, "mc_qkv_grad_pack: source %d must be non-null with 16-B aligned head rows", i);
+    src.p[i] = p->src[i]; src.sb[i] = p->sb[i]; src.sn[i] = p->sn[i]; src.sh[i] = p->sh[i];
+  }
+  MC_CHECK(p->out && aligned16(p->out) && p->ld_out % V == 0 && p->ld_out >= cols, MC_ERR_SHAPE,
+           "mc_qkv_grad_pack: out must be 16-B aligned with ld_out >= 3 * heads * head_dim");
+  MC_CHECK(!p->dbias || (p->workspace && p->workspace_bytes >= mc_grad_colsum_workspace_bytes(rows, cols)),
+           MC_ERR_WORKSPACE, "mc_qkv_grad_pack: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = p->dbias ? reinterpret_cast<float*>(p->workspace) : nullptr;
+  const int ns = grad_slices(rows);
+  const dim3 grid((unsigned)((cols / V + 63) / 64), (unsigned)ns);
+  MC_DISPATCH_T(p->dtype, hipLaunchKernelGGL((qkv_pack_colsum_kernel<T>), grid, dim3(256), 0, s, p->batch, p->seq,
+                                             p->heads, p->head_dim, src, (T*)p->out, p->ld_out, part));
+  if (p->dbias)
+    hipLaunchKernelGGL(colsum_slices_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, ns, cols, p->dbias);
+  return check_launch("mc_qkv_grad_pack");
 }
 
 extern "C" int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, int32_t P, int32_t dtype,

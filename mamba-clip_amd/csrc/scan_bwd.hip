@@ -145,7 +145,9 @@ struct ChunkRows {
   __device__ static __forceinline__ int off(int r, int c) { return r * RB + ((c ^ ((r >> kShift) & (VPR - 1))) << 4); }
 };
 
-template <typename TI, int kN, bool kAligned, bool kSP, int kMinW>
+// kDirs: grouped-direction addressing (reverse_groups / u_groups) compiled in; the plain
+// instantiation carries none of it.
+template <typename TI, int kN, bool kAligned, bool kSP, int kMinW, bool kDirs = false>
 __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
   using CR = ChunkRows<TI>;
   constexpr int VI = ElemTraits<TI>::kVec;   // elements per 16-B vector
@@ -191,8 +193,8 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
   const int64_t bs1 = wave == 0 ? a.dt_bs : a.go_bs, ds1 = wave == 0 ? a.dt_ds : a.go_ds;
   // grouped directions: reversed groups walk mirrored positions; u_groups > 0 shares u blocks
   // (vector path: the host guarantees seqlen % VI == 0, so a mirrored 16-B block is aligned)
-  const bool rev = (a.rev_groups >> g) & 1;
-  const int row0 = (a.u_groups && wave == 0) ? (g % a.u_groups) * H + dblk * kRows : dbase;
+  const bool rev = kDirs && ((a.rev_groups >> g) & 1);
+  const int row0 = (kDirs && a.u_groups && wave == 0) ? (g % a.u_groups) * H + dblk * kRows : dbase;
   const TI* rb0 = src0 + (int64_t)b * bs0 + (int64_t)row0 * ds0;
   const TI* rb1 = src1 + (int64_t)b * bs1 + (int64_t)dbase * ds1;
   const int slot0 = wave == 0 ? 0 : 2, slot1 = wave == 0 ? 1 : 3;
@@ -670,8 +672,12 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
 // Column sums over the batch: out[c] = sum_b in[b][c] (row stride ld).  A
 // block = 32 columns x 8 batch lanes; the 8 partials meet in LDS in a fixed
 // order (deterministic).  Used for dD and dbias (cols = d).
-__global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__ in, int batch, int cols, int64_t ld,
-                                                       float* __restrict__ out) {
+__global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__ in0, const float* __restrict__ in1,
+                                                       int batch, int cols, int64_t ld, float* __restrict__ out0,
+                                                       float* __restrict__ out1) {
+  // blockIdx.y selects the (slab, output) pair: dD and dbias in one launch
+  const float* __restrict__ in = blockIdx.y ? in1 : in0;
+  float* __restrict__ out = blockIdx.y ? out1 : out0;
   __shared__ float part[8][33];
   const int cx = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cx;
@@ -741,7 +747,17 @@ static int launch_bwd_n(const BwdArgs& a, bool aligned, hipStream_t s) {
   // 2 waves per SIMD where registers and LDS allow it (16-bit rows, kN <= 16): <= 256 VGPRs,
   // <= 40 KB LDS per workgroup; fp32 rows or kN = 32 run at one wave per SIMD.
   constexpr int kMinW = (sizeof(TI) == 2 && kN <= 16) ? 2 : 1;
-  if (aligned && a.softplus)
+  if (a.rev_groups || a.u_groups) {   // grouped directions (SS2D)
+    if (aligned && a.softplus)
+      hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, true, kMinW, true>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+    else if (aligned)
+      hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, false, kMinW, true>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+    else if (a.softplus)
+      hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, true, kMinW, true>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
+    else
+      hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, false, false, kMinW, true>), dim3(a.total_blocks), dim3(kWG), lds, s,
+                         a);
+  } else if (aligned && a.softplus)
     hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, true, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
   else if (aligned)
     hipLaunchKernelGGL((scan_bwd_kernel<TI, kN, true, false, kMinW>), dim3(a.total_blocks), dim3(kWG), lds, s, a);
@@ -773,12 +789,12 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
   const int ca = a.dim * a.dstate;
   hipLaunchKernelGGL(scan_bwd_colsum_nd, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, a.dim, a.dstate,
                      (int64_t)a.dim * kN, dA);
-  if (dD)
-    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_d, a.batch, a.dim,
-                       (int64_t)a.dim, dD);
-  if (dbias)
-    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, a.slab_bias, a.batch, a.dim,
-                       (int64_t)a.dim, dbias);
+  if (dD && dbias)
+    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32, 2), dim3(256), 0, s, a.slab_d, a.slab_bias, a.batch,
+                       a.dim, (int64_t)a.dim, dD, dbias);
+  else if (dD || dbias)
+    hipLaunchKernelGGL(scan_bwd_colsum, dim3((a.dim + 31) / 32), dim3(256), 0, s, dD ? a.slab_d : a.slab_bias,
+                       nullptr, a.batch, a.dim, (int64_t)a.dim, dD ? dD : dbias, nullptr);
 }
 
 template <typename TW>

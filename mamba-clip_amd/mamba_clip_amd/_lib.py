@@ -86,6 +86,15 @@ class CEFusedParams(ctypes.Structure):
     ]
 
 
+class QkvPackParams(ctypes.Structure):
+    """Mirror of ``mc_qkv_pack_params`` (include/mc_ops.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("seq", c_i32), ("heads", c_i32), ("head_dim", c_i32), ("dtype", c_i32),
+        ("src", c_vp * 3), ("sb", c_i64 * 3), ("sn", c_i64 * 3), ("sh", c_i64 * 3),
+        ("out", c_vp), ("ld_out", c_i64), ("dbias", c_fp), ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -116,7 +125,7 @@ SYMBOLS = {
     "mc_add_layernorm_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_vp, c_fp, c_fp, ctypes.c_float, c_vp, c_vp,
                                             c_fp, c_fp, c_vp]),
     "mc_add_layernorm_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_fp, c_fp, c_fp, c_vp, c_fp, c_fp,
-                                            c_vp, ctypes.c_size_t, c_vp]),
+                                            c_fp, c_vp, ctypes.c_size_t, c_vp]),
     "mc_add_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "mc_causal_conv1d_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_i64, c_fp, c_fp, c_i32,
                                             c_vp, c_i64, c_i64, c_vp]),
@@ -125,6 +134,10 @@ SYMBOLS = {
                                             ctypes.c_size_t, c_vp]),
     "mc_causal_conv1d_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_patch_im2col": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "mc_grad_colsum_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "mc_gelu_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_fp, c_vp,
+                                   ctypes.c_size_t, c_vp]),
+    "mc_qkv_grad_pack": (ctypes.c_int, [ctypes.POINTER(QkvPackParams), c_vp]),
 }
 
 _lib = None

@@ -27,8 +27,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import add_layernorm, add_rmsnorm, causal_conv1d, linear_sk, patch_im2col, wleft_mm
-from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, grouped_scan_fn,
+from .ops import (GradSlab, add_layernorm, add_rmsnorm, causal_conv1d, fc1_gelu, linear_sk, patch_im2col, qkv_proj,
+                  split_rows, wleft_mm)
+from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, SelectiveScanFn, grouped_scan_fn,
                                        selective_scan_fn)
 
 
@@ -38,6 +39,12 @@ def _dt_bias_init(d_inner, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
     dt = torch.exp(torch.rand(d_inner) * (math.log(dt_max) - math.log(dt_min)) + math.log(dt_min))
     dt = dt.clamp(min=dt_init_floor)
     return dt + torch.log(-torch.expm1(-dt))
+
+
+def mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab):
+    """The mixer's scan call (selective_scan_fn semantics, softplus on) with dz written into
+    the in_proj gradient slab."""
+    return SelectiveScanFn.apply(x, delta, A, Bm, Cm, D, z, delta_bias, True, False, dz_slab)
 
 
 class MambaMixer(nn.Module):
@@ -78,18 +85,21 @@ class MambaMixer(nn.Module):
         H = hidden.reshape(Bsz * L, dm)
         # projections: weight-left GEMMs with split-K weight gradients (ops.wleft_mm / linear_sk)
         xz = wleft_mm(self.in_proj.weight, H.t())                             # (2*di, B*L)
-        x, z = xz.split(di, dim=0)
+        # the conv / scan backward kernels write dx / dz into one (2*di, B*L) slab: the split's
+        # gradient is that slab, no concatenation (ops.GradSlab)
+        slab = GradSlab(2 * di, Bsz * L, xz.dtype, xz.device) if xz.requires_grad else None
+        x, z = split_rows(xz, di, slab)
         x = x.view(di, Bsz, L).transpose(0, 1)                                # (B, di, L) channel-major
         z = z.view(di, Bsz, L).transpose(0, 1)
-        x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True)
+        x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True, dx_slab=slab)
         x_dbl = wleft_mm(self.x_proj.weight, x.transpose(0, 1).reshape(di, Bsz * L))   # (R+2N, B*L)
         dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
         delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
         Bm = Bm.view(N, Bsz, L).transpose(0, 1)                               # (B, N, L)
         Cm = Cm.view(N, Bsz, L).transpose(0, 1)
         A = -torch.exp(self.A_log.float())
-        y = selective_scan_fn(x, delta, A, Bm, Cm, self.D.float(), z=z,
-                              delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
+        y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(),
+                       (slab, di) if slab is not None else None)
         y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
         out = linear_sk(y2.t(), self.out_proj.weight)                          # (B*L, d_model)
         return out.view(Bsz, L, dm)
@@ -196,8 +206,9 @@ class Attention(nn.Module):
         # unbind (not index) the q/k/v slices: its backward stacks the three
         # gradients in one write instead of zero-filling and accumulating a
         # (3, B, H, N, D) buffer three times and copying it contiguous again
-        q, k, v = linear_sk(x, self.qkv.weight, self.qkv.bias).view(Bsz, N, 3, self.heads, C // self.heads).unbind(2)
-        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        # q, k, v: (B, H, N, D) views of the packed qkv output; the backward packs dq / dk / dv and
+        # the qkv bias gradient in one pass (ops.QKVProjFn)
+        q, k, v = qkv_proj(x, self.qkv.weight, self.qkv.bias, self.heads)
         if x.is_cuda:
             with _gpu_sdpa_backends():
                 o = F.scaled_dot_product_attention(q, k, v)
@@ -228,7 +239,7 @@ class ViTBlock(nn.Module):
         y, h = add_layernorm(m, h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         a = self.attn(y)
         y, h = add_layernorm(a, h, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        return linear_sk(F.gelu(linear_sk(y, self.fc1.weight, self.fc1.bias)), self.fc2.weight, self.fc2.bias), h
+        return linear_sk(fc1_gelu(y, self.fc1.weight, self.fc1.bias), self.fc2.weight, self.fc2.bias), h
 
 
 class VisionTransformer(nn.Module):

@@ -195,6 +195,19 @@ def ce_fused_grad(X, Y, sc, lse_r, lse_c, row_off, coef_r, col_off, coef_c, gout
     return G, dscale
 
 
+def _mm(a, b, out):
+    """torch.mm; fp32 operands at exact fp32 (gfx950 has full-rate-for-f32 MFMA), even when the
+    process enabled TF32-class matmuls (init_device sets allow_tf32 like the reference CLI)."""
+    if a.dtype != torch.float32:
+        return torch.mm(a, b, out=out)
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        return torch.mm(a, b, out=out)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
+
+
 def _block_rows(other):
     return max(128, CE_GRAD_BLOCK_ELEMS // max(other, 1) // 128 * 128)
 
@@ -246,7 +259,7 @@ class ScaledLogitsCE(torch.autograd.Function):
                 G, ds = ce_fused_grad(Xc[r0:r1], Yc, sc, lse_r[r0:r1], lse_c, row_off + r0, coef_r, col_off - r0,
                                       coef_c, gout, gdt, want_ds)
                 if dX is not None:
-                    torch.mm(G, Yc, out=dX[r0:r1])
+                    _mm(G, Yc, dX[r0:r1])
                 if ds is not None:
                     parts.append(ds)
             if want_ds:
@@ -260,7 +273,7 @@ class ScaledLogitsCE(torch.autograd.Function):
                 # transposed problem: rows = columns c0..c1 of S, columns = rows of S
                 GT, _ = ce_fused_grad(Yc[c0:c1], Xc, sc, lse_c[c0:c1] if has_c else None, lse_r, col_off + c0,
                                       coef_c, row_off - c0, coef_r, gout, gdt)
-                torch.mm(GT, Xc, out=dY[c0:c1])
+                _mm(GT, Xc, dY[c0:c1])
             dY = dY.to(ydt)
         dS = dscale.to(sdt).reshape(sshape) if want_ds else None
         return dX, dY, dS, None, None, None, None
@@ -344,7 +357,7 @@ class AddLayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dh):
         h, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _layernorm_bwd(h, w, mean, rstd, dy, dh, ctx.meta[1] is not None)
+        dx, dw, db = _layernorm_bwd(h, w, mean, rstd, dy, dh, ctx.meta[1] is not None, want_colsum=True)
         wdt, bdt = ctx.meta
         return dx, dx, dw.to(wdt), (db.to(bdt) if db is not None else None), None
 
@@ -373,12 +386,15 @@ class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _layernorm_bwd(x, w, mean, rstd, dy, None, ctx.meta[1] is not None)
+        dx, dw, db = _layernorm_bwd(x, w, mean, rstd, dy, None, ctx.meta[1] is not None, want_colsum=True)
         wdt, bdt = ctx.meta
         return dx, dw.to(wdt), (db.to(bdt) if db is not None else None), None
 
 
-def _layernorm_bwd(h, w, mean, rstd, dy, dh, has_bias):
+COLSUM_ATTR = "_mc_colsum"   # fp32 column sums riding on a gradient tensor (LinearSK picks them up)
+
+
+def _layernorm_bwd(h, w, mean, rstd, dy, dh, has_bias, want_colsum=False):
     lib = _lib.load()
     cols = h.shape[-1]
     rows = h.numel() // cols
@@ -387,12 +403,18 @@ def _layernorm_bwd(h, w, mean, rstd, dy, dh, has_bias):
     dx = torch.empty_like(h)
     dw = torch.empty(cols, device=h.device, dtype=torch.float32)
     db = torch.empty(cols, device=h.device, dtype=torch.float32) if has_bias else None
+    csum = torch.empty(cols, device=h.device, dtype=torch.float32) if want_colsum else None
     ws_b = lib.mc_add_layernorm_bwd_workspace_bytes(rows, cols)
     ws = _ws(ws_b, h.device)
     _lib.check(lib.mc_add_layernorm_bwd(rows, cols, _lib.dtype_code(h.dtype), dy.data_ptr(), _lib.ptr(dh),
                                         h.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
-                                        dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), ws_b,
+                                        dw.data_ptr(), _lib.ptr(db), _lib.ptr(csum), ws.data_ptr(), ws_b,
                                         _lib.stream_handle(h.device)), "mc_add_layernorm_bwd")
+    if csum is not None:
+        # the bias gradient of the linear layer whose output entered this norm (fc2 / attention
+        # proj): LinearSK.backward uses it instead of re-reading dx for the column sum
+        # (with dx's version counter: an in-place accumulation into dx invalidates the sums)
+        setattr(dx, COLSUM_ATTR, (csum, dx._version))
     return dx, dw, db
 
 
@@ -403,11 +425,60 @@ def add_layernorm(x, residual, weight, bias, eps=1e-6):
     return AddLayerNormFn.apply(x, residual, weight, bias, eps)
 
 
+class GradSlab:
+    """One gradient buffer shared by the backward passes of ops that read row blocks of the
+    same channel-major activation.  The Mamba mixer splits in_proj's (2*d_inner, B*L) output
+    into x (-> conv1d) and z (-> the scan's gate); the scan backward writes dz and the conv
+    backward writes dx straight into their halves of one (2*d_inner, B*L) buffer, so the
+    split's backward is the buffer itself instead of a concatenating copy."""
+
+    def __init__(self, rows, cols, dtype, device):
+        self.rows, self.cols, self.dtype, self.device = rows, cols, dtype, device
+        self.buf = None
+
+    def get(self):
+        if self.buf is None:
+            self.buf = torch.empty(self.rows, self.cols, dtype=self.dtype, device=self.device)
+        return self.buf
+
+    def block(self, r0, r1, batch):
+        """rows [r0, r1) as the (batch, r1 - r0, L) channel-major view the kernels take."""
+        return self.get()[r0:r1].view(r1 - r0, batch, self.cols // batch).transpose(0, 1)
+
+
+class SplitRowsFn(torch.autograd.Function):
+    """(X[:k], X[k:]) of a 2-D activation; backward returns the slab when both gradients
+    already live in it (written there by the consumers' backward kernels), else concatenates."""
+
+    @staticmethod
+    def forward(ctx, X, k, slab):
+        ctx.k, ctx.slab, ctx.shape = k, slab, X.shape
+        return X[:k], X[k:]
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        k, slab = ctx.k, ctx.slab
+        buf = slab.buf if slab is not None else None
+        if (buf is not None and ga is not None and gb is not None and ga.data_ptr() == buf.data_ptr()
+                and gb.data_ptr() == buf[k:].data_ptr() and ga.stride() == buf.stride() == gb.stride()):
+            slab.shared = True   # (observable by tests: the no-copy path was taken)
+            return buf, None, None
+        rows, cols = ctx.shape
+        ref = ga if ga is not None else gb
+        ga = ga if ga is not None else torch.zeros(k, cols, dtype=ref.dtype, device=ref.device)
+        gb = gb if gb is not None else torch.zeros(rows - k, cols, dtype=ref.dtype, device=ref.device)
+        return torch.cat([ga, gb]), None, None
+
+
+def split_rows(X, k, slab=None):
+    return SplitRowsFn.apply(X, k, slab)
+
+
 class CausalConv1dFn(torch.autograd.Function):
     """Depthwise causal conv1d (+SiLU) over (batch, dim, seqlen); output contiguous."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, silu):
+    def forward(ctx, x, weight, bias, silu, dx_slab=None):
         lib = _lib.load()
         if x.stride(-1) != 1:
             x = x.contiguous()
@@ -422,6 +493,7 @@ class CausalConv1dFn(torch.autograd.Function):
                    "mc_causal_conv1d_fwd")
         ctx.save_for_backward(x, w, b if b is not None else w)
         ctx.meta = (silu, bias is not None, weight.shape, weight.dtype)
+        ctx.dx_slab = dx_slab
         return y
 
     @staticmethod
@@ -434,7 +506,8 @@ class CausalConv1dFn(torch.autograd.Function):
         dy = dy.to(x.dtype)
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
-        dx = torch.empty_like(x)
+        # dx into rows [0, D) of the shared slab (x was rows [0, D) of the in_proj output)
+        dx = ctx.dx_slab.block(0, D, Bsz) if ctx.dx_slab is not None else torch.empty_like(x)
         dw = torch.empty(D, K, device=x.device, dtype=torch.float32)
         db = torch.empty(D, device=x.device, dtype=torch.float32) if has_b else None
         ws_b = lib.mc_causal_conv1d_bwd_workspace_bytes(Bsz, D, L, K)
@@ -444,11 +517,11 @@ class CausalConv1dFn(torch.autograd.Function):
                                             dy.data_ptr(), dy.stride(0), dy.stride(1), dx.data_ptr(), dx.stride(0),
                                             dx.stride(1), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(),
                                             ws_b, _lib.stream_handle(x.device)), "mc_causal_conv1d_bwd")
-        return dx, dw.reshape(wshape).to(wdt), (db.to(wdt) if db is not None else None), None
+        return dx, dw.reshape(wshape).to(wdt), (db.to(wdt) if db is not None else None), None, None
 
 
-def causal_conv1d(x, weight, bias=None, silu=True):
-    return CausalConv1dFn.apply(x, weight, bias, silu)
+def causal_conv1d(x, weight, bias=None, silu=True, dx_slab=None):
+    return CausalConv1dFn.apply(x, weight, bias, silu, dx_slab)
 
 
 class PatchIm2colFn(torch.autograd.Function):
@@ -543,7 +616,11 @@ class LinearSK(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = wgrad(g2.t(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.sum(g2, 0, dtype=torch.float32)
+            pre = getattr(gy, COLSUM_ATTR, None)   # column sums taken by the producer of gy (LayerNorm bwd)
+            if pre is not None and pre[1] == gy._version and pre[0].shape[0] == g2.shape[1]:
+                db = pre[0]
+            else:
+                db = torch.sum(g2, 0, dtype=torch.float32)
         return dx, dw, db
 
 
@@ -580,3 +657,111 @@ class WeightLeftMM(torch.autograd.Function):
 
 def wleft_mm(weight, X):
     return WeightLeftMM.apply(weight, X)
+
+
+# ---------------------------------------------------------------------------- fused bias-gradient passes (mc_ops.h)
+def _aligned_rows(t, V):
+    return t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and t.stride(0) % V == 0
+
+
+class FC1GeluFn(torch.autograd.Function):
+    """a = gelu(x @ w^T + b) -- the MLP's first projection and activation (timm Mlp fc1 + GELU).
+
+    Backward on the GPU: one pass (mc_gelu_bwd) forms gh = ga * gelu'(h) AND the fc1 bias
+    gradient; then dx = gh @ w and the split-K weight gradient.  Elsewhere (CPU tests) the
+    same math in torch."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        dt = _compute_dtype(x)
+        xc, wc, bc = x.to(dt), weight.to(dt), bias.to(dt)
+        with torch.autocast("cuda", enabled=False):
+            h = torch.nn.functional.linear(xc, wc, bc)
+            a = torch.nn.functional.gelu(h)
+        ctx.save_for_backward(xc, wc, h)
+        return a
+
+    @staticmethod
+    def backward(ctx, ga):
+        xc, wc, h = ctx.saved_tensors
+        cols = h.shape[-1]
+        h2 = h.reshape(-1, cols)
+        g2 = ga.reshape(-1, cols).to(h.dtype)
+        V = 16 // h.element_size()
+        if h.is_cuda and cols % V == 0 and _aligned_rows(h2, V) and _aligned_rows(g2, V):
+            lib = _lib.load()
+            gh = torch.empty_like(h2)
+            db = torch.empty(cols, device=h.device, dtype=torch.float32)
+            ws_b = lib.mc_grad_colsum_workspace_bytes(h2.shape[0], cols)
+            ws = _ws(ws_b, h.device)
+            _lib.check(lib.mc_gelu_bwd(h2.shape[0], cols, _lib.dtype_code(h.dtype), h2.data_ptr(), h2.stride(0),
+                                       g2.data_ptr(), g2.stride(0), gh.data_ptr(), gh.stride(0), db.data_ptr(),
+                                       ws.data_ptr(), ws_b, _lib.stream_handle(h.device)), "mc_gelu_bwd")
+        else:
+            gh = torch.ops.aten.gelu_backward(g2, h2)
+            db = gh.sum(0, dtype=torch.float32)
+        x2 = xc.reshape(-1, xc.shape[-1])
+        dx = torch.mm(gh, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dw = wgrad(gh.t(), x2) if ctx.needs_input_grad[1] else None
+        return dx, dw, db if ctx.needs_input_grad[2] else None
+
+
+def fc1_gelu(x, weight, bias):
+    return FC1GeluFn.apply(x, weight, bias)
+
+
+class QKVProjFn(torch.autograd.Function):
+    """(q, k, v) = heads of x @ w^T + b, each (B, H, N, D) -- a view of the (B, N, 3, H, D) output.
+
+    Backward on the GPU: mc_qkv_grad_pack writes dq / dk / dv straight into the packed
+    (B*N, 3C) output gradient and sums its columns (the qkv bias gradient) in the same pass --
+    no stack copy, no second read; then dx and the split-K weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, heads):
+        dt = _compute_dtype(x)
+        xc, wc, bc = x.to(dt), weight.to(dt), bias.to(dt)
+        Bsz, N, C = xc.shape
+        with torch.autocast("cuda", enabled=False):
+            y = torch.nn.functional.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.heads = heads
+        q, k, v = y.view(Bsz, N, 3, heads, C // heads).unbind(2)
+        return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        xc, wc = ctx.saved_tensors
+        Bsz, N, C = xc.shape
+        H = ctx.heads
+        D = C // H
+        grads = [g if g is not None else torch.zeros(Bsz, H, N, D, device=xc.device, dtype=xc.dtype)
+                 for g in (dq, dk, dv)]
+        grads = [g.to(xc.dtype) for g in grads]
+        V = 16 // xc.element_size()
+        ok = xc.is_cuda and D % V == 0 and all(
+            g.stride(-1) == 1 and g.data_ptr() % 16 == 0 and all(st % V == 0 for st in g.stride()[:3]) for g in grads)
+        if ok:
+            lib = _lib.load()
+            g2 = torch.empty(Bsz * N, 3 * C, device=xc.device, dtype=xc.dtype)
+            db = torch.empty(3 * C, device=xc.device, dtype=torch.float32)
+            p = _lib.QkvPackParams()
+            p.batch, p.seq, p.heads, p.head_dim, p.dtype = Bsz, N, H, D, _lib.dtype_code(xc.dtype)
+            for i, g in enumerate(grads):          # g: (B, H, N, D) -> strides of batch, token, head
+                p.src[i] = g.data_ptr()
+                p.sb[i], p.sn[i], p.sh[i] = g.stride(0), g.stride(2), g.stride(1)
+            ws_b = lib.mc_grad_colsum_workspace_bytes(Bsz * N, 3 * C)
+            ws = _ws(ws_b, xc.device)
+            p.out, p.ld_out, p.dbias = g2.data_ptr(), 3 * C, db.data_ptr()
+            p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+            _lib.check(lib.mc_qkv_grad_pack(p, _lib.stream_handle(xc.device)), "mc_qkv_grad_pack")
+        else:
+            g2 = torch.stack([g.transpose(1, 2) for g in grads], dim=2).reshape(Bsz * N, 3 * C)
+            db = g2.sum(0, dtype=torch.float32)
+        dx = torch.mm(g2, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dw = wgrad(g2.t(), xc.reshape(-1, C)) if ctx.needs_input_grad[1] else None
+        return dx, dw, db if ctx.needs_input_grad[2] else None, None
+
+
+def qkv_proj(x, weight, bias, heads):
+    return QKVProjFn.apply(x, weight, bias, heads)

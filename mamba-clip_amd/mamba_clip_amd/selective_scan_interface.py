@@ -108,7 +108,7 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None):
     """Run mc_scan_bwd.  With ``dirs``, du comes back per group, (B, dim, L): the caller sums the
     groups that share a u block."""
     lib = _lib.load()
@@ -118,7 +118,7 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
     dout = _last_dim_contig(dout)
     du = torch.empty_like(u) if dirs is None else torch.empty_like(delta)
     ddelta = torch.empty_like(delta)
-    dz = torch.empty_like(z) if z is not None else None
+    dz = (dz_out if dz_out is not None else torch.empty_like(z)) if z is not None else None
     dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
     dC = torch.empty(C.shape, device=u.device, dtype=C.dtype)
     dA = torch.empty(dim, dstate, device=u.device, dtype=torch.float32)
@@ -158,7 +158,7 @@ class SelectiveScanFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
-                return_last_state=False):
+                return_last_state=False, dz_slab=None):
         u, delta, z = _last_dim_contig(u), _last_dim_contig(delta), _last_dim_contig(z)
         squeeze_B, squeeze_C = B.dim() == 3, C.dim() == 3
         B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
@@ -176,13 +176,18 @@ class SelectiveScanFn(torch.autograd.Function):
         ctx.dtypes = (A.dtype, D.dtype if D is not None else None,
                       delta_bias.dtype if delta_bias is not None else None)
         ctx.has = (D is not None, z is not None, delta_bias is not None)
+        ctx.dz_slab = dz_slab   # (GradSlab, first row): dz written into that slab (ops.GradSlab)
         return (out, last) if return_last_state else out
 
     @staticmethod
     def backward(ctx, dout, *args):
         u, delta, A32, B, C, D32, z, bias32, states = ctx.saved_tensors
+        dz_out = None
+        if ctx.dz_slab is not None and z is not None:
+            slab, r0 = ctx.dz_slab
+            dz_out = slab.block(r0, r0 + z.shape[1], z.shape[0])
         du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, delta, A32, B, C, D32, z, bias32,
-                                                         ctx.delta_softplus, dout, states)
+                                                         ctx.delta_softplus, dout, states, dz_out=dz_out)
         if ctx.squeeze[0]:
             dB = dB.squeeze(1)
         if ctx.squeeze[1]:
@@ -192,7 +197,7 @@ class SelectiveScanFn(torch.autograd.Function):
                 dD.to(d_dt) if dD is not None else None,
                 dz,
                 dbias.to(b_dt) if dbias is not None else None,
-                None, None)
+                None, None, None)
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,

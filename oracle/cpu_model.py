@@ -23,7 +23,7 @@ def _add_rmsnorm_f32(x, res, w, eps=1e-5):
     return y.to(x.dtype), h
 
 
-def _causal_conv1d_f32(x, w, b=None, silu=True):
+def _causal_conv1d_f32(x, w, b=None, silu=True, dx_slab=None):
     D, K = w.shape[0], w.shape[-1]
     y = F.conv1d(x, w.reshape(D, 1, K).to(x.dtype), b.to(x.dtype) if b is not None else None,
                  padding=K - 1, groups=D)[..., : x.shape[-1]]
@@ -62,7 +62,11 @@ def grouped_scan_ref(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=
     return torch.stack([fl(out[:, g], g) for g in range(G)], 1).reshape(Bsz, dim, L)
 
 
-_OPS = {"selective_scan_fn": selective_scan_ref, "grouped_scan_fn": grouped_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
+def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab):
+    return selective_scan_ref(x, delta, A, Bm, Cm, D, z=z, delta_bias=delta_bias, delta_softplus=True)
+
+
+_OPS = {"selective_scan_fn": selective_scan_ref, "mixer_scan": _mixer_scan, "grouped_scan_fn": grouped_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
         "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col, "add_layernorm": _add_layernorm_f32}
 
 

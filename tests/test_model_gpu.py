@@ -97,6 +97,83 @@ def test_vit_block_matches_unfused_math():
     torch.testing.assert_close(out.detach(), ref, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fc1_gelu_fused_backward(dt):
+    """mc_gelu_bwd (gh = ga * gelu'(h) + the fc1 bias gradient in one pass) vs torch's unfused
+    GELU backward + sum, same weights, fp32 and bf16 (rows not a multiple of the slice size)."""
+    from mamba_clip_amd.ops import fc1_gelu
+    torch.manual_seed(3)
+    x = torch.randn(5, 77, 96, device=DEV).to(dt).requires_grad_(True)
+    w = (0.1 * torch.randn(256, 96, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(256, device=DEV)).requires_grad_(True)
+    ga = torch.randn(5, 77, 256, device=DEV).to(dt)
+    a = fc1_gelu(x, w, b)
+    a.backward(ga)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    h = F.linear(xr, wr.to(dt), br.to(dt))
+    ar = F.gelu(h)
+    ar.backward(ga)
+    tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(a, ar, **tol)
+    torch.testing.assert_close(x.grad, xr.grad, **tol)
+    torch.testing.assert_close(w.grad, wr.grad, **(dict(rtol=1e-4, atol=1e-4) if dt == torch.float32
+                                                   else dict(rtol=2e-2, atol=5e-2)))
+    # the bias gradient: sum of the stored gh (bf16-rounded for bf16) -- vs torch's gelu_backward output summed
+    gh = torch.ops.aten.gelu_backward(ga.reshape(-1, 256), h.detach().reshape(-1, 256))
+    # bf16: an element of gh may round one ulp apart from torch's (erf evaluated differently)
+    btol = dict(rtol=1e-5, atol=1e-4) if dt == torch.float32 else dict(rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(b.grad, gh.sum(0, dtype=torch.float32), **btol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_qkv_proj_fused_pack(dt):
+    """mc_qkv_grad_pack packs the attention's dq / dk / dv (strides as SDPA returns them) into the
+    qkv output gradient and sums the qkv bias gradient: vs linear + unbind + stack."""
+    from mamba_clip_amd.ops import qkv_proj
+    torch.manual_seed(4)
+    Bsz, N, C, H = 3, 50, 128, 4
+    x = torch.randn(Bsz, N, C, device=DEV).to(dt).requires_grad_(True)
+    w = (0.05 * torch.randn(3 * C, C, device=DEV)).requires_grad_(True)
+    b = (0.05 * torch.randn(3 * C, device=DEV)).requires_grad_(True)
+    go = torch.randn(Bsz, H, N, C // H, device=DEV).to(dt)
+    q, k, v = qkv_proj(x, w, b, H)
+    F.scaled_dot_product_attention(q, k, v).backward(go)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    qr, kr, vr = F.linear(xr, wr.to(dt), br.to(dt)).view(Bsz, N, 3, H, C // H).unbind(2)
+    F.scaled_dot_product_attention(qr.transpose(1, 2), kr.transpose(1, 2), vr.transpose(1, 2)).backward(go)
+    # bf16: torch's reference bias / weight gradients are rounded to bf16 before the fp32 cast
+    tol = dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=1e-2, atol=2e-2)
+    for got, want in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        torch.testing.assert_close(got, want, **tol)
+
+
+def test_vit_bias_grads_from_layernorm_colsum():
+    """fc2 / attention-proj bias gradients come from the column sums the LayerNorm backward takes
+    of dx (mc_add_layernorm_bwd dx_colsum); they equal the direct column sums of the gradient."""
+    from mamba_clip_amd import ops
+    from mamba_clip_amd.model import VisionTransformer
+    torch.manual_seed(5)
+    vit = VisionTransformer(img_size=32, patch=8, width=64, layers=3, heads=4, output_dim=16).to(DEV)
+    img = torch.randn(4, 3, 32, 32, device=DEV)
+    seen = []
+    orig = ops.LinearSK.backward
+
+    def spy(ctx, gy):
+        pre = getattr(gy, ops.COLSUM_ATTR, None)
+        out = orig(ctx, gy)
+        if pre is not None and pre[1] == gy._version:
+            seen.append(float((out[2] - gy.reshape(-1, gy.shape[-1]).sum(0, dtype=torch.float32)).abs().max()))
+        return out
+
+    ops.LinearSK.backward = staticmethod(spy)
+    try:
+        vit(img).square().sum().backward()
+    finally:
+        ops.LinearSK.backward = orig
+    # fc2 of blocks 0..1 and the attention proj of every block feed a following add+LayerNorm
+    assert len(seen) >= 5 and max(seen) < 1e-4, seen
+
+
 def test_causal_conv1d_fwd_bwd():
     from mamba_clip_amd.ops import causal_conv1d
     g = torch.Generator().manual_seed(1)
@@ -220,6 +297,42 @@ def test_mamba_mixer_matches_oracle():
     hr = h.detach().cpu().double().requires_grad_(True)
     R.mamba_mixer_ref(m, hr).sum().backward()
     torch.testing.assert_close(h.grad.cpu().double(), hr.grad, rtol=1e-3, atol=1e-4)
+
+
+def test_mamba_mixer_xz_gradient_slab_no_concat():
+    """The conv / scan backward kernels write dx / dz into one slab: the in_proj split's gradient
+    is that slab (no concatenation), with the same in_proj weight gradient as the copying path."""
+    from mamba_clip_amd import ops
+    from mamba_clip_amd.model import MambaMixer
+    torch.manual_seed(1)
+    m = MambaMixer(64, d_state=16).to(DEV)
+    h = torch.randn(3, 48, 64, device=DEV, requires_grad=True)
+    made = []
+    orig = ops.GradSlab.__init__
+
+    def spy(self, *a, **k):
+        orig(self, *a, **k)
+        made.append(self)
+
+    ops.GradSlab.__init__ = spy
+    try:
+        m(h).square().sum().backward()
+    finally:
+        ops.GradSlab.__init__ = orig
+    assert len(made) == 1 and getattr(made[0], "shared", False)
+    g_slab, gh_slab = m.in_proj.weight.grad.clone(), h.grad.clone()
+    # the same step with the slab disabled (plain concatenation)
+    m.zero_grad()
+    h.grad = None
+    import mamba_clip_amd.model as M
+    real = M.GradSlab
+    M.GradSlab = lambda *a, **k: None
+    try:
+        m(h).square().sum().backward()
+    finally:
+        M.GradSlab = real
+    torch.testing.assert_close(m.in_proj.weight.grad, g_slab, rtol=0, atol=0)
+    torch.testing.assert_close(h.grad, gh_slab, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("fname", ["ss2d_d32_h6w5.safetensors", "ss2d_d16_h4w4.safetensors"])
