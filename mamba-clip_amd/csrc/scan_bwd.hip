@@ -121,17 +121,6 @@ __device__ __forceinline__ float wave_transpose_reduce(float (&v)[NV], int lane)
   return v[0] + dpp_f(v[0], 3);         // lane bit 0 via quad_perm [1,0,3,2]
 }
 
-// Workgroup barrier for LDS hand-offs only: this wave's LDS operations are
-// complete, global loads / stores stay in flight (gfx950 has the back-off
-// barrier, so s_barrier itself forces no vmcnt drain; __syncthreads()'s fence
-// would wait for every prefetch still in flight).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 // LDS image of one array's chunk rows: 64 rows x RB bytes, 16-B blocks XOR-
 // swizzled by row so that 64 lanes reading their own rows at one column hit
 // distinct bank groups (ds_read_b128 lane groups) and the staging writes

@@ -31,6 +31,17 @@ inline size_t bct_bytes(int batch, int seqlen, int dstate, int n_groups) {
 static_assert(kRows == 64, "wave_lds_sync() is only valid for one-wave workgroups");
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations are
+// complete, global loads / stores stay in flight (gfx950 has the back-off
+// barrier, so s_barrier itself forces no vmcnt drain; __syncthreads()'s fence
+// would wait for every prefetch still in flight).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Lane id the compiler cannot hoist or CSE (asm volatile): values derived from
 // it are rebuilt where used instead of occupying VGPRs across a hot loop.
 __device__ __forceinline__ int opaque_lane_id() {

@@ -54,7 +54,9 @@ struct FwdArgs {
 // kAligned: 0 = element-wise rows, 1 = 16-B aligned rows, 2 = aligned and every chunk
 // full (seqlen % kT == 0: no masked-load code at all, which keeps the register
 // budget of the 3-waves-per-SIMD build free of spills)
-template <typename TI, int kN, int kAligned, int kG, bool kPBC, bool kPU, int kMinW>
+// kSP: softplus on delta (a template flag: a runtime one is a uniform branch per position
+// that splits the recurrence into small basic blocks)
+template <typename TI, int kN, int kAligned, int kG, bool kPBC, bool kPU, int kMinW, bool kSP>
 __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a) {
   using RL = RowLayout<TI>;
   constexpr int VI = RL::VI;                    // elements per 16-B vector
@@ -74,7 +76,6 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
   const int nrows = min(kRows, H - dblk * kRows);
   const int L_ = a.seqlen;
   const bool hasZ = a.z != nullptr;
-  const bool softplus = a.softplus != 0;
 
   const TI* __restrict__ u = reinterpret_cast<const TI*>(a.u) + (int64_t)b * a.u_bs;
   // grouped directions: reversed groups walk mirrored positions; u_groups > 0 shares u blocks
@@ -271,9 +272,17 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
           const int t = l0 + t0 + e;
           const float uv = uu[e];
           const float dr = dd[e] + biasv;
-          float dt = softplus ? softplus_f(dr) : dr;
-          dt = (t < L_) ? dt : 0.f;  // past the end: state frozen
+          float dt = kSP ? softplus_f(dr) : dr;
+          if constexpr (kAligned != 2) dt = (t < L_) ? dt : 0.f;  // past the end: state frozen
           const float du = dt * uv;
+          // every decay of this position first: each exp's result is consumed a
+          // few pairs later, so no wait states sit between an exp and its use
+          f32x2 dA[kN / 2];
+#pragma unroll
+          for (int p = 0; p < kN / 2; ++p) {
+            const f32x2 arg = A2[p] * dt;                                   // v_pk_mul_f32
+            dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+          }
           f32x2 y2 = {0.f, 0.f};
           {
             const f32x4* bc4 = reinterpret_cast<const f32x4*>(bcl + (t0 + e) * (2 * kN));
@@ -284,9 +293,7 @@ __global__ __launch_bounds__(kRows, kMinW) void scan_fwd_kernel(const FwdArgs a)
               for (int h = 0; h < 2; ++h) {
                 const int p = 2 * n4 + h;
                 const f32x2 bb = h ? bq.hi : bq.lo, cc = h ? cq.hi : cq.lo;
-                const f32x2 arg = A2[p] * dt;                               // v_pk_mul_f32
-                const f32x2 dA = {fast_exp2(arg.x), fast_exp2(arg.y)};
-                x[p] = dA * x[p] + bb * du;                                 // v_pk_mul + v_pk_fma
+                x[p] = dA[p] * x[p] + bb * du;                              // v_pk_mul + v_pk_fma
                 y2 = cc * x[p] + y2;                                        // v_pk_fma
               }
             }
@@ -657,13 +664,13 @@ static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
   };
   const bool span32 = fits(a.o_ds) && fits(a.u_ds) && fits(a.dt_ds) && (!a.z || fits(a.z_ds)) &&
                       (!a.out_y || fits(a.y_ds));
-  if (aligned && a.seqlen % kT == 0 && span32)
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 2, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  else if (aligned)
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 1, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s, a);
-  else
-    hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, 0, kG, kPBC, kPU, kMinW>), dim3(a.total_blocks), dim3(kRows), lds, s,
-                       a);
+#define MC_FWD_LAUNCH(AL, SP) \
+  hipLaunchKernelGGL((scan_fwd_kernel<TI, kN, AL, kG, kPBC, kPU, kMinW, SP>), dim3(a.total_blocks), dim3(kRows), lds, s, a)
+  const bool sp = a.softplus != 0;
+  if (aligned && a.seqlen % kT == 0 && span32) { if (sp) MC_FWD_LAUNCH(2, true); else MC_FWD_LAUNCH(2, false); }
+  else if (aligned) { if (sp) MC_FWD_LAUNCH(1, true); else MC_FWD_LAUNCH(1, false); }
+  else { if (sp) MC_FWD_LAUNCH(0, true); else MC_FWD_LAUNCH(0, false); }
+#undef MC_FWD_LAUNCH
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
@@ -671,11 +678,14 @@ static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
 
 // Kernel choice, measured on MI355X (tools/ab_scan_fwd.sh; ms, bf16, z, softplus):
 //                                         C4 64x3072x4096   C2 256x1536x80
-//   scan_fwd_kernel (kG 4, LDS B/C, 2 w/SIMD)     3.35             0.204
+//   scan_fwd_kernel (kG 4, LDS B/C, 2 w/SIMD)     3.17 (r01: 3.35) 0.204
 //   scan_fwd_mc_kernel R=1 (SGPR B/C, 16-pos)     3.87             0.152
 //   scan_fwd_mc_kernel R=3 (1 w/SIMD)             3.66             0.180
 // Rejected (kept in git history): per-position LDS broadcast at 3 w/SIMD
-// 3.96 / 0.188; two-wave state split with SGPR half-rows 6.41 / 0.266;
+// 3.96 / 0.188; two-wave state split with SGPR half-rows 6.41 / 0.266; two-wave
+// state split with LDS-staged rows and LDS partial-y sums (no 2+1 tail: 6
+// half-tasks per SIMD) 3.92 at C4 -- the per-position work both waves repeat
+// (row reads, softplus, y hand-off) costs more than the tail it removes;
 // vector-load B/C rings spill at the occupancy they need.  With short
 // sequences the grid is many short-lived waves and the SGPR-fed kernel wins;
 // with long ones the LDS-staged kernel's deeper prefetch wins.
