@@ -129,6 +129,18 @@ struct RowLayout {
   static constexpr int kStride = kBytes + 16;
 };
 
+// Forward kernel arguments (scan_fwd.hip, scan_fwd_pair.hip).
+struct FwdArgs {
+  int batch, dim, seqlen, dstate, n_groups, n_chunks, n_states, nblk, total_blocks;
+  int softplus;
+  int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, o_bs, o_ds;
+  const void* u; const void* delta; const float* A; const float* bct;
+  const float* D; const void* z; const float* delta_bias;
+  void* out; float* chunk_states; float* last_state;
+  void* out_y; int64_t y_bs, y_ds;   // nullable: pre-gate y + D u (training with z: the backward's dz input)
+  int rev_groups, u_groups;          // grouped directions (0 = off; element-wise path only)
+};
+
 int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who);
 bool vec_ok(const void* p, int64_t s0, int64_t s1, int64_t s2, int elem_bytes);
 

@@ -31,16 +31,10 @@
 namespace mc {
 namespace scan {
 
-struct FwdArgs {
-  int batch, dim, seqlen, dstate, n_groups, n_chunks, n_states, nblk, total_blocks;
-  int softplus;
-  int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, o_bs, o_ds;
-  const void* u; const void* delta; const float* A; const float* bct;
-  const float* D; const void* z; const float* delta_bias;
-  void* out; float* chunk_states; float* last_state;
-  void* out_y; int64_t y_bs, y_ds;   // nullable: pre-gate y + D u (training with z: the backward's dz input)
-  int rev_groups, u_groups;          // grouped directions (0 = off; element-wise path only)
-};
+// FwdArgs: scan_common.h
+bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes);   // scan_fwd_pair.hip
+int launch_fwd_pair(const FwdArgs& a, int itype, int min_waves, hipStream_t s);
+
 
 // Variants (template knobs, chosen on the host):
 //   kG     steps per group of the recurrence loop: the B/C values of a group
@@ -828,6 +822,11 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
     if (p->itype == MC_DTYPE_F32) return launch_fwd_dirs<float>(a, al, s);
     if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
     return launch_fwd_dirs<f16_t>(a, al, s);
+  }
+  {   // long sequences: state-split lane pairs (scan_fwd_pair.hip); 20 / 21 force it at 3 / 4 waves per SIMD
+    const int v = fwd_variant();
+    if (fwd_pair_ok(a, aligned, ib) && (v == 20 || v == 21 || (v < 0 && p->seqlen > 512)))
+      return launch_fwd_pair(a, p->itype, v == 21 ? 4 : 3, s);
   }
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);

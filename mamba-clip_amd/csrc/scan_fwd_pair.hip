@@ -1,0 +1,295 @@
+// scan_fwd_pair.hip -- selective-scan forward for long sequences, state-split lane pairs.
+//
+// Same op as scan_fwd.hip (reference semantics /root/reference/src/mamba_clip/model.py:83-169):
+//   dt_t = softplus(delta_t + delta_bias[d]);  x_t[n] = exp(dt_t A[d,n]) x_{t-1}[n] + dt_t B_t[n] u_t
+//   y_t  = sum_n C_t[n] x_t[n] + D[d] u_t;     out_t = y_t * silu(z_t)
+//
+// Why a second long-sequence kernel: at C4 (B 64, D 3072) the one-channel-per-lane
+// kernel has 3072 one-wave workgroups = 3 per SIMD with 2 resident, so every SIMD
+// runs a 2 + 1 round and the last third of the grid issues from a lone wave.  Here
+// a wave owns 32 channels and lane (2c + h) keeps states [8h, 8h + 8) of channel c:
+//  * 6144 waves at C4 = 6 per SIMD, half the per-lane state registers -> 3 resident,
+//    two full rounds, no lone-wave tail;
+//  * the per-position scalars are computed ONCE per (channel, position) in the
+//    cooperative staging pass, vectorised along the sequence: dt = softplus(delta +
+//    bias) and du = dt u go to LDS as fp32 pairs, so the pair never repeats them;
+//  * the two lanes of a channel read the same (dt, du) (one broadcast address per
+//    pair) and their own half of B_t / C_t (two broadcast addresses per wave);
+//  * each lane writes its partial y_t over the (dt, du) bytes it consumed; the gate
+//    pass (same vector mapping as the staging, so it still holds u for D u) adds the
+//    two partials, applies silu(z) and stores 16-B vectors along the sequence.
+// Requirements (host-checked): dstate == 16, 16-B aligned rows, seqlen % 32 == 0,
+// row spans < 2 GiB (32-bit buffer offsets), no grouped directions.
+#include "scan_common.h"
+
+namespace mc {
+namespace scan {
+
+constexpr int kPCh = 32;   // channels per wave
+constexpr int kPN = 16;    // dstate
+constexpr int kPH = 8;     // states per lane
+constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
+
+// Packed (two positions) softplus and silu: the arithmetic around the transcendental
+// ops runs as v_pk_* (one issue for two positions).  softplus keeps torch's
+// threshold (x > 20 -> x) and log1p(t) ~ t for t < 1e-4 (relative error < t / 2);
+// exp2 overflow past x = 88 gives inf, which the threshold select discards.
+__device__ __forceinline__ f32x2 softplus2(f32x2 x) {
+  const f32x2 arg = x * kLog2e;
+  const f32x2 t = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+  const f32x2 tp = t + 1.f;
+  const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)} * kLn2;
+  return f32x2{x.x > 20.f ? x.x : (t.x < 1e-4f ? t.x : lg.x), x.y > 20.f ? x.y : (t.y < 1e-4f ? t.y : lg.y)};
+}
+__device__ __forceinline__ f32x2 silu2(f32x2 z) {
+  const f32x2 arg = z * -kLog2e;
+  const f32x2 ep = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)} + 1.f;
+  return z * f32x2{fast_rcp(ep.x), fast_rcp(ep.y)};
+}
+
+template <typename TI>
+struct PairLayout {
+  static constexpr int VI = ElemTraits<TI>::kVec;  // elements per 16-B vector
+  static constexpr int kVPR = kT / VI;             // vectors per row and chunk
+  static constexpr int kNV = kPCh * kVPR / 64;     // vectors per lane and array
+  static constexpr int kStride = kT * 8 + 16;      // row: kT x {dt, du} fp32 + pad (rows on distinct banks)
+  static constexpr int kRowBytes = kPCh * kStride;
+  static constexpr int kBCBytes = kT * 2 * kPN * 4;
+};
+
+template <typename TI, bool kSP, int kMinW>
+__global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
+  using PL = PairLayout<TI>;
+  constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
+  constexpr int kBCVec = PL::kBCBytes / 16;     // float4s of one B/C chunk
+  constexpr int kBCPer = kBCVec / 64;
+  static_assert(kBCVec % 64 == 0, "B/C chunk must split evenly over the lanes");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* rowbuf = smem;
+  float* bcl = reinterpret_cast<float*>(smem + PL::kRowBytes);   // [kT][B 16 | C 16]
+
+  const int lane = threadIdx.x;
+  const int ch = lane >> 1, h = lane & 1;
+  const int lin = xcd_remap(blockIdx.x, a.total_blocks);
+  const int dblk = lin % a.nblk;
+  const int bg = lin / a.nblk;
+  const int g = bg % a.n_groups, b = bg / a.n_groups;
+  const int H = a.dim / a.n_groups;
+  const int dbase = g * H + dblk * kPCh;
+  const int nrows = min(kPCh, H - dblk * kPCh);
+  const int L_ = a.seqlen;
+  const bool hasZ = a.z != nullptr;
+
+  auto rows_rsrc = [&](const void* base, int64_t bs, int64_t ds) {
+    return make_rsrc(reinterpret_cast<const TI*>(base) + (int64_t)b * bs + (int64_t)dbase * ds,
+                     (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)));
+  };
+  const __amdgpu_buffer_rsrc_t rs_u = rows_rsrc(a.u, a.u_bs, a.u_ds);
+  const __amdgpu_buffer_rsrc_t rs_d = rows_rsrc(a.delta, a.dt_bs, a.dt_ds);
+  const __amdgpu_buffer_rsrc_t rs_z = rows_rsrc(hasZ ? a.z : a.u, hasZ ? a.z_bs : a.u_bs, hasZ ? a.z_ds : a.u_ds);
+  const __amdgpu_buffer_rsrc_t rs_o = rows_rsrc(a.out, a.o_bs, a.o_ds);
+  const __amdgpu_buffer_rsrc_t rs_y =
+      rows_rsrc(a.out_y ? a.out_y : a.u, a.out_y ? a.y_bs : a.u_bs, a.out_y ? a.y_ds : a.u_ds);
+  const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(a.bct + (int64_t)bg * L_ * (2 * kPN), (uint32_t)L_ * (2 * kPN) * 4u);
+
+  // ---- recurrence lane constants: channel ch, states [8h, 8h + 8)
+  const bool my_ok = ch < nrows;
+  const int my_dc = dbase + min(ch, nrows - 1);
+  f32x2 A2[kPH / 2];
+#pragma unroll
+  for (int p = 0; p < kPH / 2; ++p) {
+    const float* ap = a.A + (int64_t)my_dc * kPN + kPH * h + 2 * p;
+    A2[p] = my_ok ? f32x2{ap[0] * kLog2e, ap[1] * kLog2e} : f32x2{0.f, 0.f};
+  }
+  // ---- staging / gate lane constants: vector j = lane + 64 k -> row j / kVPR, block j % kVPR
+  float biasv[kNV], Dv[kNV];
+#pragma unroll
+  for (int k = 0; k < kNV; ++k) {
+    const int r = min((lane + 64 * k) / kVPR, nrows - 1);
+    biasv[k] = a.delta_bias ? a.delta_bias[dbase + r] : 0.f;
+    Dv[k] = a.D ? a.D[dbase + r] : 0.f;
+  }
+  auto voff = [&](int k, int64_t ds, int l0) {   // byte offset of this lane's vector k at chunk l0
+    const int j = lane + 64 * k;
+    const int r = min(j / kVPR, nrows - 1);
+    return (uint32_t)(r * ds + l0 + (j % kVPR) * VI) * (uint32_t)sizeof(TI);
+  };
+
+  f32x2 x[kPH / 2];
+#pragma unroll
+  for (int p = 0; p < kPH / 2; ++p) x[p] = f32x2{0.f, 0.f};
+
+  uint4 pu[kNV], pd[kNV];
+  float4 pbc[kBCPer];
+  auto load_next = [&](int l0) {   // past the end: offsets fall outside the buffer ranges and read 0
+#pragma unroll
+    for (int k = 0; k < kNV; ++k) {
+      pu[k] = buf_ld16(rs_u, voff(k, a.u_ds, l0));
+      pd[k] = buf_ld16(rs_d, voff(k, a.dt_ds, l0));
+    }
+#pragma unroll
+    for (int k = 0; k < kBCPer; ++k)
+      pbc[k] = __builtin_bit_cast(float4, buf_ld16(rs_bc, (uint32_t)(l0 * (2 * kPN) + 4 * (lane + 64 * k)) * 4u));
+  };
+
+  load_next(0);
+  for (int c0 = 0; c0 < a.n_chunks; ++c0) {
+    const int l0 = c0 * kT;
+    // ---- staging: dt = softplus(delta + bias), du = dt u as fp32 pairs; B/C chunk
+    uint4 ucur[kNV];
+#pragma unroll
+    for (int k = 0; k < kNV; ++k) {
+      const int j = lane + 64 * k;
+      char* dst = rowbuf + (j / kVPR) * PL::kStride + (j % kVPR) * VI * 8;
+      ucur[k] = pu[k];
+#pragma unroll
+      for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
+        const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
+        const f32x2 dt = kSP ? softplus2(dr) : dr;
+        const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
+        reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, du.x, dt.y, du.y);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kBCPer; ++k) reinterpret_cast<float4*>(bcl)[lane + 64 * k] = pbc[k];
+    wave_lds_sync();
+    load_next(l0 + kT);
+    uint4 cz[kNV];
+    if (hasZ) {
+#pragma unroll
+      for (int k = 0; k < kNV; ++k) cz[k] = buf_ld16(rs_z, voff(k, a.z_ds, l0));
+    }
+
+    // ---- recurrence: 8 states of one channel per lane, groups of kPG positions.  The
+    // next position's B/C halves and the next group's {dt, du} are read one step
+    // ahead (software pipeline), so the LDS latency sits under the current step.
+    {
+      const char* row = rowbuf + ch * PL::kStride;
+      const f32x4* bcp = reinterpret_cast<const f32x4*>(bcl + kPH * h);   // position stride 2kN floats = 8 f32x4
+      f32x4 nb0 = bcp[0], nb1 = bcp[1], nc0 = bcp[kPN / 4], nc1 = bcp[kPN / 4 + 1];
+      f32x4 nq0 = *reinterpret_cast<const f32x4*>(row), nq1 = *reinterpret_cast<const f32x4*>(row + 16);
+#pragma unroll 2
+      for (int t0 = 0; t0 < kT; t0 += kPG) {
+        const f32x4 q0 = nq0, q1 = nq1;
+        {
+          const int tn = (t0 + kPG) & (kT - 1);   // (last group: wraps to an unused re-read)
+          nq0 = *reinterpret_cast<const f32x4*>(row + tn * 8);
+          nq1 = *reinterpret_cast<const f32x4*>(row + tn * 8 + 16);
+        }
+        const float dtv[kPG] = {q0.x, q0.z, q1.x, q1.z};
+        const float duv[kPG] = {q0.y, q0.w, q1.y, q1.w};
+        float yv[kPG];
+#pragma unroll
+        for (int e = 0; e < kPG; ++e) {
+          const float dt = dtv[e], du = duv[e];
+          const f32x4 b0 = nb0, b1 = nb1, c0v = nc0, c1v = nc1;
+          {
+            const f32x4* np = bcp + ((t0 + e + 1) & (kT - 1)) * (2 * kPN / 4);
+            nb0 = np[0]; nb1 = np[1]; nc0 = np[kPN / 4]; nc1 = np[kPN / 4 + 1];
+          }
+          f32x2 dA[kPH / 2];
+#pragma unroll
+          for (int p = 0; p < kPH / 2; ++p) {
+            const f32x2 arg = A2[p] * dt;                                   // v_pk_mul_f32
+            dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+          }
+          x[0] = dA[0] * x[0] + b0.lo * du;                                  // v_pk_mul + v_pk_fma
+          x[1] = dA[1] * x[1] + b0.hi * du;
+          x[2] = dA[2] * x[2] + b1.lo * du;
+          x[3] = dA[3] * x[3] + b1.hi * du;
+          f32x2 y2 = c0v.lo * x[0];
+          y2 = c0v.hi * x[1] + y2;
+          y2 = c1v.lo * x[2] + y2;
+          y2 = c1v.hi * x[3] + y2;
+          yv[e] = y2.x + y2.y;
+        }
+        // partial y over the {dt, du} bytes both lanes of the pair have consumed
+        *reinterpret_cast<float4*>(const_cast<char*>(row) + t0 * 8 + 16 * h) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+      }
+    }
+    if (a.chunk_states && my_ok && c0 < a.n_states) {   // state after position l0 + kT - 1 (kS == kT)
+      float4* cs = reinterpret_cast<float4*>(a.chunk_states +
+                                             (((int64_t)b * a.dim + dbase + ch) * a.n_states + c0) * kPN + kPH * h);
+      cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
+      cs[1] = make_float4(x[2].x, x[2].y, x[3].x, x[3].y);
+    }
+    wave_lds_sync();
+
+    // ---- gate + store: y = y_h0 + y_h1 + D u, out = y silu(z), coalesced 16-B vectors
+#pragma unroll
+    for (int k = 0; k < kNV; ++k) {
+      const int j = opaque_lane_id() + 64 * k;
+      const int r = j / kVPR;
+      const char* src = rowbuf + r * PL::kStride + (j % kVPR) * VI * 8;
+      float o[VI];
+#pragma unroll
+      for (int gi = 0; gi < VI / kPG; ++gi) {
+        const f32x4 ya = reinterpret_cast<const f32x4*>(src)[2 * gi];
+        const f32x4 yb = reinterpret_cast<const f32x4*>(src)[2 * gi + 1];
+#pragma unroll
+        for (int i = 0; i < kPG; i += 2) {
+          const int e = gi * kPG + i;
+          const f32x2 uu = f32x2{elem_f<TI>(ucur[k], e), elem_f<TI>(ucur[k], e + 1)};
+          const f32x2 y = Dv[k] * uu + (f32x2{ya[i], ya[i + 1]} + f32x2{yb[i], yb[i + 1]});
+          o[e] = y.x;
+          o[e + 1] = y.y;
+        }
+      }
+      const uint32_t ob = r < nrows ? 0u : 0x80000000u;   // rows past the group end: out of range, dropped
+      if (hasZ) {
+        if (a.out_y) buf_st16(rs_y, voff(k, a.y_ds, l0) | ob, pack_f<TI>(o));
+#pragma unroll
+        for (int e = 0; e < VI; e += 2) {
+          const f32x2 g = silu2(f32x2{elem_f<TI>(cz[k], e), elem_f<TI>(cz[k], e + 1)}) * f32x2{o[e], o[e + 1]};
+          o[e] = g.x;
+          o[e + 1] = g.y;
+        }
+      }
+      buf_st16(rs_o, voff(k, a.o_ds, l0) | ob, pack_f<TI>(o));
+    }
+    wave_lds_sync();   // next chunk's staging overwrites the rows
+  }
+
+  if (a.last_state && my_ok) {
+    float4* ls = reinterpret_cast<float4*>(a.last_state + ((int64_t)b * a.dim + dbase + ch) * kPN + kPH * h);
+    ls[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
+    ls[1] = make_float4(x[2].x, x[2].y, x[3].x, x[3].y);
+  }
+}
+
+// Eligibility of the pair kernel for a (validated) forward call.
+bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes) {
+  auto fits = [&](int64_t ds) {
+    return ((int64_t)(kPCh - 1) * (ds < 0 ? -ds : ds) + a.seqlen) * itype_bytes < ((int64_t)1 << 31);
+  };
+  return itype_bytes == 2 && aligned && a.dstate == kPN && a.seqlen % kT == 0 && kS == kT && a.rev_groups == 0 && a.u_groups == 0 &&
+         fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) && (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds));
+}
+
+template <typename TI, int kMinW>
+static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
+  FwdArgs a = a0;
+  const int H = a.dim / a.n_groups;
+  a.nblk = (H + kPCh - 1) / kPCh;
+  a.total_blocks = a.batch * a.n_groups * a.nblk;
+  const size_t lds = (size_t)PairLayout<TI>::kRowBytes + PairLayout<TI>::kBCBytes;
+  if (a.softplus)
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
+  else
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+// 16-bit rows only (fp32 rows double the staging registers and spill at 3 waves / SIMD);
+// occupancy: waves per SIMD the register budget is sized for (3 or 4)
+int launch_fwd_pair(const FwdArgs& a, int itype, int min_waves, hipStream_t s) {
+  if (itype == MC_DTYPE_BF16)
+    return min_waves >= 4 ? launch_pair_t<bf16_t, 4>(a, s) : launch_pair_t<bf16_t, 3>(a, s);
+  return min_waves >= 4 ? launch_pair_t<f16_t, 4>(a, s) : launch_pair_t<f16_t, 3>(a, s);
+}
+
+}  // namespace scan
+}  // namespace mc

@@ -77,6 +77,9 @@ CASES = [
     # add one fully masked tile past L
     (2, 192, 40, 16, 1, torch.bfloat16, torch.bfloat16, True, False),      # 5 tiles (odd)
     (2, 128, 24, 16, 2, torch.float16, torch.bfloat16, False, False),      # 3 tiles, no z, G=2
+    # long sequences take the state-split pair kernel (scan_fwd_pair.hip): ragged 32-channel blocks
+    (2, 96, 1024, 16, 2, torch.bfloat16, torch.bfloat16, True, False),     # H=48: a full + a half block
+    (1, 80, 544, 16, 1, torch.float16, torch.float32, False, False),       # 17 chunks, no z, H=80
 ]
 
 
