@@ -106,7 +106,7 @@ def scan_roofline(iters, warmup=3):
     del u, z, delta, Bm, Cm
     torch.cuda.empty_cache()
     traffic, traffic_src = _pmc_traffic()
-    return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
+    return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_pair_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "traffic_measured_in_this_run": False,

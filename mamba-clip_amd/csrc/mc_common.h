@@ -70,8 +70,18 @@ __device__ __forceinline__ uint4 pack16_impl(const float (&v)[8]) {
   return make_uint4(bits16<T>(v[0]) | (bits16<T>(v[1]) << 16), bits16<T>(v[2]) | (bits16<T>(v[3]) << 16),
                     bits16<T>(v[4]) | (bits16<T>(v[5]) << 16), bits16<T>(v[6]) | (bits16<T>(v[7]) << 16));
 }
-template <> __device__ __forceinline__ uint4 pack_f<bf16_t>(const float (&v)[8]) { return pack16_impl<bf16_t>(v); }
-template <> __device__ __forceinline__ uint4 pack_f<f16_t>(const float (&v)[8]) { return pack16_impl<f16_t>(v); }
+// 16-bit outputs convert two values per instruction (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32, RNE)
+template <typename T>
+__device__ __forceinline__ uint32_t cvt_pk2(float a, float b) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), t2));
+}
+template <typename T>
+__device__ __forceinline__ uint4 pack16_pk(const float (&v)[8]) {
+  return make_uint4(cvt_pk2<T>(v[0], v[1]), cvt_pk2<T>(v[2], v[3]), cvt_pk2<T>(v[4], v[5]), cvt_pk2<T>(v[6], v[7]));
+}
+template <> __device__ __forceinline__ uint4 pack_f<bf16_t>(const float (&v)[8]) { return pack16_pk<bf16_t>(v); }
+template <> __device__ __forceinline__ uint4 pack_f<f16_t>(const float (&v)[8]) { return pack16_pk<f16_t>(v); }
 
 // raw 16-bit/32-bit element bits
 template <typename T> __device__ __forceinline__ uint32_t ld_bits(const T* p) {

@@ -32,14 +32,16 @@ constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} p
 
 // Packed (two positions) softplus and silu: the arithmetic around the transcendental
 // ops runs as v_pk_* (one issue for two positions).  softplus keeps torch's
-// threshold (x > 20 -> x) and log1p(t) ~ t for t < 1e-4 (relative error < t / 2);
-// exp2 overflow past x = 88 gives inf, which the threshold select discards.
+// threshold (x > 20 -> x) with one median instead of two selects.
 __device__ __forceinline__ f32x2 softplus2(f32x2 x) {
-  const f32x2 arg = x * kLog2e;
+  const f32x2 arg = f32x2{fminf(x.x, 20.f), fminf(x.y, 20.f)} * kLog2e;
   const f32x2 t = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
   const f32x2 tp = t + 1.f;
   const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)} * kLn2;
-  return f32x2{x.x > 20.f ? x.x : (t.x < 1e-4f ? t.x : lg.x), x.y > 20.f ? x.y : (t.y < 1e-4f ? t.y : lg.y)};
+  // x < lg < t holds for every x <= 20 (log1p(t) < t, log1p(e^x) > x), so the median is
+  // lg there; above 20 (t clamped to e^20, lg ~ 20) it is x: torch's threshold.  For
+  // x < -9 it is min(lg, t): lg can lose ~1e-7 absolute to the rounding of 1 + t.
+  return f32x2{__builtin_amdgcn_fmed3f(x.x, lg.x, t.x), __builtin_amdgcn_fmed3f(x.y, lg.y, t.y)};
 }
 __device__ __forceinline__ f32x2 silu2(f32x2 z) {
   const f32x2 arg = z * -kLog2e;
@@ -52,7 +54,7 @@ struct PairLayout {
   static constexpr int VI = ElemTraits<TI>::kVec;  // elements per 16-B vector
   static constexpr int kVPR = kT / VI;             // vectors per row and chunk
   static constexpr int kNV = kPCh * kVPR / 64;     // vectors per lane and array
-  static constexpr int kStride = kT * 8 + 16;      // row: kT x {dt, du} fp32 + pad (rows on distinct banks)
+  static constexpr int kStride = kT * 8 + 16;      // row: per 2 positions {dt, dt, du, du} fp32 + pad (rows on distinct banks)
   static constexpr int kRowBytes = kPCh * kStride;
   static constexpr int kBCBytes = kT * 2 * kPN * 4;
 };
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
         const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
         const f32x2 dt = kSP ? softplus2(dr) : dr;
         const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
-        reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, du.x, dt.y, du.y);
+        reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, dt.y, du.x, du.y);
       }
     }
 #pragma unroll
@@ -177,8 +179,8 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           nq0 = *reinterpret_cast<const f32x4*>(row + tn * 8);
           nq1 = *reinterpret_cast<const f32x4*>(row + tn * 8 + 16);
         }
-        const float dtv[kPG] = {q0.x, q0.z, q1.x, q1.z};
-        const float duv[kPG] = {q0.y, q0.w, q1.y, q1.w};
+        const float dtv[kPG] = {q0.x, q0.y, q1.x, q1.y};
+        const float duv[kPG] = {q0.z, q0.w, q1.z, q1.w};
         float yv[kPG];
 #pragma unroll
         for (int e = 0; e < kPG; ++e) {

@@ -14,6 +14,7 @@ ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--noz", action="store_true")
 ap.add_argument("--bwd", action="store_true", help="time forward+backward (training) instead")
+ap.add_argument("--train-fwd", action="store_true", help="time the training forward (saves the chunk states)")
 ap.add_argument("--cm", action="store_true",
                 help="channel-major views like the Mamba mixer: (B, D, L) with strides (L, B*L, 1)")
 args = ap.parse_args()
@@ -44,6 +45,9 @@ if args.bwd:
 
 
 def step():
+    if args.train_fwd:
+        from mamba_clip_amd.selective_scan_interface import scan_fwd
+        return scan_fwd(u, delta, A, Bm, Cm, Dv, z, bias, True, True, False)
     out = selective_scan_fn(u, delta, A, Bm, Cm, Dv, z, bias, delta_softplus=True)
     if args.bwd:
         out.backward(g_out)
@@ -61,5 +65,5 @@ torch.cuda.synchronize()
 ms = s.elapsed_time(e) / args.iters
 es = u.element_size()
 nbytes = Bsz * D * L * es * (4 if z is not None else 3) + 2 * Bsz * N * L * es + (D * N + 2 * D) * 4
-print(f"shape {args.shape} {args.dtype} z={z is not None} bwd={args.bwd}: {ms:.3f} ms  {nbytes / ms / 1e6:.1f} GB/s "
+print(f"shape {args.shape} {args.dtype} z={z is not None} bwd={args.bwd} train_fwd={args.train_fwd}: {ms:.3f} ms  {nbytes / ms / 1e6:.1f} GB/s "
       f"({nbytes / ms / 1e6 / 8000 * 100:.1f}% of 8 TB/s)")
