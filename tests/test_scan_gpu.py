@@ -158,6 +158,10 @@ def test_scan_fwd_empty_and_errors():
     with pytest.raises(RuntimeError):
         B1 = torch.randn(1, 1, 16, 10, device=DEV)
         selective_scan_fn(u, u.half(), A, B1, B1)
+    # dstate above MC_SCAN_MAX_DSTATE (32) is rejected, not run on a slow path
+    with pytest.raises(RuntimeError):
+        B64 = torch.randn(1, 1, 64, 10, device=DEV)
+        selective_scan_fn(u, u, -torch.ones(64, 64, device=DEV), B64, B64)
 
 
 # ----------------------------------------------------------------- backward
