@@ -823,9 +823,10 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
     if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
     return launch_fwd_dirs<f16_t>(a, al, s);
   }
-  {   // long sequences: state-split lane pairs (scan_fwd_pair.hip); 20 / 21 force it at 3 / 4 waves per SIMD
+  {   // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
+      // forward 0.166 vs 0.183 ms per layer); 20 / 21 force it at 3 / 4 waves per SIMD
     const int v = fwd_variant();
-    if (fwd_pair_ok(a, aligned, ib) && (v == 20 || v == 21 || (v < 0 && p->seqlen > 512)))
+    if (fwd_pair_ok(a, aligned, ib) && (v == 20 || v == 21 || v < 0))
       return launch_fwd_pair(a, p->itype, v == 21 ? 4 : 3, s);
   }
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);

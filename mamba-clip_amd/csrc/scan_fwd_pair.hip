@@ -18,8 +18,10 @@
 //  * each lane writes its partial y_t over the (dt, du) bytes it consumed; the gate
 //    pass (same vector mapping as the staging, so it still holds u for D u) adds the
 //    two partials, applies silu(z) and stores 16-B vectors along the sequence.
-// Requirements (host-checked): dstate == 16, 16-B aligned rows, seqlen % 32 == 0,
+// Requirements (host-checked): dstate == 16, 16-B aligned 16-bit rows, seqlen % 8 == 0,
 // row spans < 2 GiB (32-bit buffer offsets), no grouped directions.
+#include <type_traits>
+
 #include "scan_common.h"
 
 namespace mc {
@@ -138,21 +140,30 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
   load_next(0);
   for (int c0 = 0; c0 < a.n_chunks; ++c0) {
     const int l0 = c0 * kT;
-    // ---- staging: dt = softplus(delta + bias), du = dt u as fp32 pairs; B/C chunk
+    // ---- staging: dt = softplus(delta + bias), du = dt u as fp32 pairs; B/C chunk.  In a
+    // chunk that runs past the end (L % kT != 0; L % VI == 0, so whole vectors) the vectors
+    // at positions >= L stage dt = du = 0: the state stays frozen, the saved state is the one
+    // after L - 1.  A uniform branch picks the masked copy, full chunks carry no selects.
     uint4 ucur[kNV];
+    auto stage = [&](auto masked) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < kNV; ++k) {
-      const int j = lane + 64 * k;
-      char* dst = rowbuf + (j / kVPR) * PL::kStride + (j % kVPR) * VI * 8;
-      ucur[k] = pu[k];
+      for (int k = 0; k < kNV; ++k) {
+        const int j = lane + 64 * k;
+        char* dst = rowbuf + (j / kVPR) * PL::kStride + (j % kVPR) * VI * 8;
+        ucur[k] = pu[k];
+        const bool vok = !decltype(masked)::value || l0 + (j % kVPR) * VI < L_;
 #pragma unroll
-      for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
-        const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
-        const f32x2 dt = kSP ? softplus2(dr) : dr;
-        const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
-        reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, dt.y, du.x, du.y);
+        for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
+          const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
+          f32x2 dt = kSP ? softplus2(dr) : dr;
+          if constexpr (decltype(masked)::value) dt = vok ? dt : f32x2{0.f, 0.f};
+          const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
+          reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, dt.y, du.x, du.y);
+        }
       }
-    }
+    };
+    if (l0 + kT <= L_) stage(std::false_type());
+    else stage(std::true_type());
 #pragma unroll
     for (int k = 0; k < kBCPer; ++k) reinterpret_cast<float4*>(bcl)[lane + 64 * k] = pbc[k];
     wave_lds_sync();
@@ -238,7 +249,8 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           o[e + 1] = y.y;
         }
       }
-      const uint32_t ob = r < nrows ? 0u : 0x80000000u;   // rows past the group end: out of range, dropped
+      // rows past the group end and vectors past L: out of range, dropped
+      const uint32_t ob = (r < nrows && l0 + (j % kVPR) * VI < L_) ? 0u : 0x80000000u;
       if (hasZ) {
         if (a.out_y) buf_st16(rs_y, voff(k, a.y_ds, l0) | ob, pack_f<TI>(o));
 #pragma unroll
@@ -265,7 +277,7 @@ bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes) {
   auto fits = [&](int64_t ds) {
     return ((int64_t)(kPCh - 1) * (ds < 0 ? -ds : ds) + a.seqlen) * itype_bytes < ((int64_t)1 << 31);
   };
-  return itype_bytes == 2 && aligned && a.dstate == kPN && a.seqlen % kT == 0 && kS == kT && a.rev_groups == 0 && a.u_groups == 0 &&
+  return itype_bytes == 2 && aligned && a.dstate == kPN && a.seqlen % 8 == 0 && kS == kT && a.rev_groups == 0 && a.u_groups == 0 &&
          fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) && (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds));
 }
 

@@ -80,6 +80,7 @@ CASES = [
     # long sequences take the state-split pair kernel (scan_fwd_pair.hip): ragged 32-channel blocks
     (2, 96, 1024, 16, 2, torch.bfloat16, torch.bfloat16, True, False),     # H=48: a full + a half block
     (1, 80, 544, 16, 1, torch.float16, torch.float32, False, False),       # 17 chunks, no z, H=80
+    (2, 64, 1000, 16, 1, torch.bfloat16, torch.bfloat16, True, False),     # last chunk runs past L (masked)
 ]
 
 
