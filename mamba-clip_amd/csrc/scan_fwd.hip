@@ -33,7 +33,7 @@ namespace scan {
 
 // FwdArgs: scan_common.h
 bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes);   // scan_fwd_pair.hip
-int launch_fwd_pair(const FwdArgs& a, int itype, int min_waves, hipStream_t s);
+int launch_fwd_pair(const FwdArgs& a, int itype, int variant, hipStream_t s);
 
 
 // Variants (template knobs, chosen on the host):
@@ -824,10 +824,10 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
     return launch_fwd_dirs<f16_t>(a, al, s);
   }
   {   // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
-      // forward 0.166 vs 0.183 ms per layer); 20 / 21 force it at 3 / 4 waves per SIMD
+      // forward 0.166 vs 0.183 ms per layer); 20-23 force it (variants: scan_fwd_pair.hip)
     const int v = fwd_variant();
-    if (fwd_pair_ok(a, aligned, ib) && (v == 20 || v == 21 || v < 0))
-      return launch_fwd_pair(a, p->itype, v == 21 ? 4 : 3, s);
+    if (fwd_pair_ok(a, aligned, ib) && (v < 0 || (v >= 20 && v <= 23)))
+      return launch_fwd_pair(a, p->itype, v, s);
   }
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);

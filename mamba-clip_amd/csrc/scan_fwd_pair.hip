@@ -45,6 +45,33 @@ __device__ __forceinline__ f32x2 softplus2(f32x2 x) {
   // x < -9 it is min(lg, t): lg can lose ~1e-7 absolute to the rounding of 1 + t.
   return f32x2{__builtin_amdgcn_fmed3f(x.x, lg.x, t.x), __builtin_amdgcn_fmed3f(x.y, lg.y, t.y)};
 }
+__device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
+  // softplus(x) = max(x, 0) + log1p(exp(-|x|)): exp never overflows, and above 20 the log1p
+  // term is below half an ulp of x, which is torch's threshold (x > 20 -> x) exactly.
+  // -|arg| is a free VOP3 input modifier on v_exp_f32.
+  const f32x2 arg = x * kLog2e;
+  const f32x2 t = f32x2{fast_exp2(-fabsf(arg.x)), fast_exp2(-fabsf(arg.y))};
+  const f32x2 tp = t + 1.f;
+  const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)};
+  return lg * kLn2 + f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
+}
+// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
+  f32x2 r;
+  if constexpr (kHi) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  return r;
+}
+// a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
+// (the compiler otherwise moves an odd-register scalar to an even register first)
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
+  f32x2 r;
+  if constexpr (kHi) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(s));
+  else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(s));
+  return r;
+}
 __device__ __forceinline__ f32x2 silu2(f32x2 z) {
   const f32x2 arg = z * -kLog2e;
   const f32x2 ep = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)} + 1.f;
@@ -61,7 +88,7 @@ struct PairLayout {
   static constexpr int kBCBytes = kT * 2 * kPN * 4;
 };
 
-template <typename TI, bool kSP, int kMinW>
+template <typename TI, bool kSP, int kMinW, int kVar>
 __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
   using PL = PairLayout<TI>;
   constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
@@ -155,7 +182,7 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
 #pragma unroll
         for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
           const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
-          f32x2 dt = kSP ? softplus2(dr) : dr;
+          f32x2 dt = kSP ? (kVar >= 1 ? softplus2_log1p(dr) : softplus2(dr)) : dr;
           if constexpr (decltype(masked)::value) dt = vok ? dt : f32x2{0.f, 0.f};
           const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
           reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, dt.y, du.x, du.y);
@@ -201,16 +228,37 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
             const f32x4* np = bcp + ((t0 + e + 1) & (kT - 1)) * (2 * kPN / 4);
             nb0 = np[0]; nb1 = np[1]; nc0 = np[kPN / 4]; nc1 = np[kPN / 4 + 1];
           }
+          __builtin_amdgcn_sched_barrier(0);   // keep the reads a step ahead (the scheduler sinks them to their use)
           f32x2 dA[kPH / 2];
 #pragma unroll
           for (int p = 0; p < kPH / 2; ++p) {
-            const f32x2 arg = A2[p] * dt;                                   // v_pk_mul_f32
+            f32x2 arg;
+            if constexpr (kVar >= 2)   // dt broadcast from its half of the {dt, dt} register pair
+              arg = (e & 1) ? pk_mul_bcast<1>(A2[p], e < 2 ? q0.xy : q1.xy)
+                            : pk_mul_bcast<0>(A2[p], e < 2 ? q0.xy : q1.xy);
+            else
+              arg = A2[p] * dt;                                             // v_pk_mul_f32
             dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
           }
-          x[0] = dA[0] * x[0] + b0.lo * du;                                  // v_pk_mul + v_pk_fma
-          x[1] = dA[1] * x[1] + b0.hi * du;
-          x[2] = dA[2] * x[2] + b1.lo * du;
-          x[3] = dA[3] * x[3] + b1.hi * du;
+          if constexpr (kVar >= 2) {   // du broadcast from its half of {du, du}
+            const f32x2 dup = e < 2 ? q0.zw : q1.zw;
+            if (e & 1) {
+              x[0] = pk_fma_bcast<1>(b0.lo, dup, dA[0] * x[0]);
+              x[1] = pk_fma_bcast<1>(b0.hi, dup, dA[1] * x[1]);
+              x[2] = pk_fma_bcast<1>(b1.lo, dup, dA[2] * x[2]);
+              x[3] = pk_fma_bcast<1>(b1.hi, dup, dA[3] * x[3]);
+            } else {
+              x[0] = pk_fma_bcast<0>(b0.lo, dup, dA[0] * x[0]);
+              x[1] = pk_fma_bcast<0>(b0.hi, dup, dA[1] * x[1]);
+              x[2] = pk_fma_bcast<0>(b1.lo, dup, dA[2] * x[2]);
+              x[3] = pk_fma_bcast<0>(b1.hi, dup, dA[3] * x[3]);
+            }
+          } else {
+            x[0] = dA[0] * x[0] + b0.lo * du;                                // v_pk_mul + v_pk_fma
+            x[1] = dA[1] * x[1] + b0.hi * du;
+            x[2] = dA[2] * x[2] + b1.lo * du;
+            x[3] = dA[3] * x[3] + b1.hi * du;
+          }
           f32x2 y2 = c0v.lo * x[0];
           y2 = c0v.hi * x[1] + y2;
           y2 = c1v.lo * x[2] + y2;
@@ -281,7 +329,7 @@ bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes) {
          fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) && (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds));
 }
 
-template <typename TI, int kMinW>
+template <typename TI, int kMinW, int kVar>
 static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   FwdArgs a = a0;
   const int H = a.dim / a.n_groups;
@@ -289,20 +337,26 @@ static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   a.total_blocks = a.batch * a.n_groups * a.nblk;
   const size_t lds = (size_t)PairLayout<TI>::kRowBytes + PairLayout<TI>::kBCBytes;
   if (a.softplus)
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, kVar>), dim3(a.total_blocks), dim3(64), lds, s, a);
   else
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, kVar>), dim3(a.total_blocks), dim3(64), lds, s, a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }
 
-// 16-bit rows only (fp32 rows double the staging registers and spill at 3 waves / SIMD);
-// occupancy: waves per SIMD the register budget is sized for (3 or 4)
-int launch_fwd_pair(const FwdArgs& a, int itype, int min_waves, hipStream_t s) {
-  if (itype == MC_DTYPE_BF16)
-    return min_waves >= 4 ? launch_pair_t<bf16_t, 4>(a, s) : launch_pair_t<bf16_t, 3>(a, s);
-  return min_waves >= 4 ? launch_pair_t<f16_t, 4>(a, s) : launch_pair_t<f16_t, 3>(a, s);
+// 16-bit rows only (fp32 rows double the staging registers and spill at 3 waves / SIMD).
+// variant (A/B builds, MC_SCAN_FWD_VARIANT; interleaved on one box, tools/ab_pair_variants.sh, C4 ms):
+// 20 median softplus 2.82, 21 = 20 at 4 waves/SIMD (spills) 3.59, 22 log1p softplus 2.80,
+// 23 (default) = 22 + op_sel broadcasts of dt / du in inline asm 2.78; one-channel kernel 3.26
+int launch_fwd_pair(const FwdArgs& a, int itype, int variant, hipStream_t s) {
+  if (itype == MC_DTYPE_BF16) {
+    if (variant == 21) return launch_pair_t<bf16_t, 4, 0>(a, s);
+    if (variant == 20) return launch_pair_t<bf16_t, 3, 0>(a, s);
+    if (variant == 22) return launch_pair_t<bf16_t, 3, 1>(a, s);
+    return launch_pair_t<bf16_t, 3, 2>(a, s);
+  }
+  return launch_pair_t<f16_t, 3, 2>(a, s);
 }
 
 }  // namespace scan
