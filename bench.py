@@ -105,12 +105,36 @@ def scan_roofline(iters, warmup=3):
     achieved = nbytes / (ms * 1e-3) / 1e9
     del u, z, delta, Bm, Cm
     torch.cuda.empty_cache()
+    copy_gbs = _copy_bandwidth(dev)
     traffic, traffic_src = _pmc_traffic()
     return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_pair_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "traffic_measured_in_this_run": False,
-            "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes}
+            "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes,
+            # also report the achievable copy bandwidth measured on this box
+            "copy_gbs_measured": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 4)}
+
+
+def _copy_bandwidth(dev, nbytes=2 << 30, iters=10):
+    """Device-to-device copy rate (read + write bytes / time) of a 2 GiB buffer, HIP events."""
+    import torch
+    src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device=dev).normal_()
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    stream = torch.cuda.current_stream(dev)
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    t0.record(stream)
+    for _ in range(iters):
+        dst.copy_(src)
+    t1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = t0.elapsed_time(t1) / iters
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def similarity_c5(iters=20, warmup=3):
