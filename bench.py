@@ -39,6 +39,13 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (MI355X_MICROARCH.md)
 MFMA_BF16_DENSE_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 MFMA_FP8_DENSE_TFLOPS = 5000.0   # dense fp8 MFMA peak (no sparsity)
 C2_FLOP_PER_PAIR = 146e9         # fwd+bwd, SURVEY.md 8(d)
+# per-model workload labels and fwd+bwd FLOP per pair (C2 146 G, C3 243 G)
+WORKLOADS = {
+    "vit_b16-mamba130m": ("C2: ViT-B/16 image + Mamba-130M text, contrastive train step (fwd+bwd+AdamW), amp_bf16",
+                          C2_FLOP_PER_PAIR),
+    "biomedclip-vit_b16-pubmedbert256": ("C3: BiomedCLIP ViT-B/16 image + PubMedBERT-256 text, contrastive train "
+                                         "step (fwd+bwd+AdamW), amp_bf16", 243e9),
+}
 
 
 def parse():
@@ -289,6 +296,9 @@ def main():
     median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1]
                                                                              + step_ms[len(step_ms) // 2])
     value = world * args.batch * args.steps / elapsed
+    seq_len = int(inner.text.context_length)
+    workload, flop_pair = WORKLOADS.get(args.model, (f"{args.model}: contrastive train step (fwd+bwd+AdamW), "
+                                                     "amp_bf16", C2_FLOP_PER_PAIR))
     result = {
         "metric": "image-text pairs/sec (whole node) + selective_scan HBM GB/s",
         "value": round(value, 2), "unit": "image-text pairs/sec", "n_gpus": world,
@@ -296,17 +306,16 @@ def main():
         "median_ms_per_step": round(median_ms, 3),
         "median_pairs_per_sec": round(world * args.batch / (median_ms * 1e-3), 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) 77-token text, EOT last)",
-        "config": {"workload": "C2: ViT-B/16 image + Mamba-130M text, contrastive train step "
-                               "(fwd+bwd+AdamW), amp_bf16",
+        "data": f"synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) {seq_len}-token text, EOT last)",
+        "config": {"workload": workload,
                    "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                   "seq_len": int(inner.text.context_length), "image_size": 224,
+                   "seq_len": seq_len, "image_size": 224,
                    "parallelism": f"dp{world}",
                    "library_gemm_selection": "tunableop-file" if gemm_tuned else "default-heuristic"},
-        "mfma_estimate": {"flop_per_pair": C2_FLOP_PER_PAIR,
-                          "achieved_tflops_per_gpu": round(value / world * C2_FLOP_PER_PAIR / 1e12, 1),
+        "mfma_estimate": {"flop_per_pair": flop_pair,
+                          "achieved_tflops_per_gpu": round(value / world * flop_pair / 1e12, 1),
                           "peak": MFMA_BF16_DENSE_TFLOPS,
-                          "frac": round(value / world * C2_FLOP_PER_PAIR / 1e12 / MFMA_BF16_DENSE_TFLOPS, 4)},
+                          "frac": round(value / world * flop_pair / 1e12 / MFMA_BF16_DENSE_TFLOPS, 4)},
         "final_loss": round(final_loss, 5),
     }
     del images, texts, targets, optimizer
