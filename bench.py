@@ -77,8 +77,12 @@ def relaunch(args):
     return subprocess.call(cmd)
 
 
-def scan_roofline(iters, warmup=3):
-    """selective_scan_fwd at C4 timed with HIP events on its launch stream."""
+def scan_roofline(iters, warmup=10):
+    """selective_scan_fwd at C4 timed with HIP events on its launch stream.
+
+    10 untimed calls first: right after the MFMA-heavy training steps the first ~8 calls run
+    slower (rocprof trace, profiles/r02: 3.5 -> 2.6 ms while the clocks settle), and the
+    roofline is about the kernel's steady state."""
     import torch
     from mamba_clip_amd.selective_scan_interface import scan_fwd
     dev = torch.device("cuda", torch.cuda.current_device())
