@@ -1,4 +1,5 @@
-// scan_fwd_pair.hip -- selective-scan forward for long sequences, state-split lane pairs.
+// scan_fwd_pair.hip -- selective-scan forward with state-split lane pairs (every 16-bit, N = 16 call:
+// the C2 and C4 text towers).
 //
 // Same op as scan_fwd.hip (reference semantics /root/reference/src/mamba_clip/model.py:83-169):
 //   dt_t = softplus(delta_t + delta_bias[d]);  x_t[n] = exp(dt_t A[d,n]) x_{t-1}[n] + dt_t B_t[n] u_t
@@ -33,8 +34,9 @@ constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
 
 // Packed (two positions) softplus and silu: the arithmetic around the transcendental
-// ops runs as v_pk_* (one issue for two positions).  softplus keeps torch's
-// threshold (x > 20 -> x) with one median instead of two selects.
+// ops runs as v_pk_* (one issue for two positions).  Both softplus forms keep torch's
+// threshold (x > 20 -> x) without selects; softplus2_log1p is the default (variant 23),
+// softplus2 (one median) the A/B variant 20.
 __device__ __forceinline__ f32x2 softplus2(f32x2 x) {
   const f32x2 arg = f32x2{fminf(x.x, 20.f), fminf(x.y, 20.f)} * kLog2e;
   const f32x2 t = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
@@ -55,14 +57,6 @@ __device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
   const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)};
   return lg * kLn2 + f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
 }
-// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
-template <int kHi>
-__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
-  f32x2 r;
-  if constexpr (kHi) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
-  else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
-  return r;
-}
 // a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
 // (the compiler otherwise moves an odd-register scalar to an even register first)
 template <int kHi>
@@ -70,6 +64,14 @@ __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
   f32x2 r;
   if constexpr (kHi) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(s));
   else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(s));
+  return r;
+}
+// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
+  f32x2 r;
+  if constexpr (kHi) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
   return r;
 }
 __device__ __forceinline__ f32x2 silu2(f32x2 z) {
