@@ -650,8 +650,13 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
     const int l = (int)(r % L);
     const int64_t bgi = r / L;
     if (n >= dstate) continue;
+    // the slab rows of one output are L * 2kN floats apart: keep 8 loads in flight
+    // (the sum order stays k = 0, 1, 2, ...: deterministic, as before)
+    const float* sp = slab + (bgi * nblk * L + l) * (2 * kN) + which * kN + n;
+    const int64_t kst = (int64_t)L * (2 * kN);
     float s = 0.f;
-    for (int k = 0; k < nblk; ++k) s += slab[((bgi * nblk + k) * L + l) * (2 * kN) + which * kN + n];
+#pragma unroll 8
+    for (int k = 0; k < nblk; ++k) s += sp[k * kst];
     TW* dst = which ? dC : dB;
     const int lo = ((rev >> (int)(bgi % G)) & 1) ? L - 1 - l : l;
     dst[(bgi * dstate + n) * L + lo] = from_f<TW>(s);
