@@ -677,6 +677,7 @@ __global__ __launch_bounds__(256) void scan_bwd_colsum(const float* __restrict__
   const int c = blockIdx.x * 32 + cx;
   float s = 0.f;
   if (c < cols)
+#pragma unroll 8   // loads in flight; the summation order is unchanged
     for (int bb = q; bb < batch; bb += 8) s += in[(int64_t)bb * ld + c];
   part[q][cx] = s;
   __syncthreads();
@@ -698,6 +699,7 @@ __global__ __launch_bounds__(256) void scan_bwd_colsum_nd(const float* __restric
   const int cols = dim * dstate;
   float s = 0.f;
   if (c < cols)
+#pragma unroll 8   // loads in flight; the summation order is unchanged
     for (int bb = q; bb < batch; bb += 8) s += in[(int64_t)bb * ld + c];
   part[q][cx] = s;
   __syncthreads();
