@@ -174,6 +174,7 @@ __global__ __launch_bounds__(256) void colsum_pass1_kernel(const float* __restri
   const int per = (nrows + kColSlices - 1) / kColSlices;
   const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
   float s = 0.f;
+#pragma unroll 8   // loads in flight; the summation order is unchanged
   for (int r = r0; r < r1; ++r) s += in[(int64_t)r * cols + c];
   tmp[(int64_t)blockIdx.y * cols + c] = s;
 }
@@ -731,6 +732,7 @@ __global__ __launch_bounds__(256) void colsum_slices_kernel(const float* __restr
   const int c = blockIdx.x * 32 + cx;
   float s = 0.f;
   if (c < cols)
+#pragma unroll 8   // loads in flight; the summation order is unchanged
     for (int k = q; k < nslices; k += 8) s += part[(int64_t)k * cols + c];
   red[q][cx] = s;
   __syncthreads();
