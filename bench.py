@@ -59,8 +59,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may run on (see _cpu_threads)")
     return ap.parse_args()
 
 
@@ -128,21 +129,30 @@ def scan_roofline(iters, warmup=10):
 
 
 def _copy_bandwidth(dev, nbytes=2 << 30, iters=10):
-    """Device-to-device copy rate (read + write bytes / time) of a 2 GiB buffer, HIP events."""
+    """Achievable streaming rate: the library's float4 non-temporal copy kernel (mc_stream_copy,
+    include/mc_ops.h) over a 2 GiB buffer, read + write bytes / time, HIP events on its stream.
+    (MI355X_MICROARCH.md measures 6.29 TB/s for a float4 copy; torch's copy_ runs slower.)"""
     import torch
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
     src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device=dev).normal_()
     dst = torch.empty_like(src)
-    for _ in range(2):
-        dst.copy_(src)
     stream = torch.cuda.current_stream(dev)
+    h = _lib.stream_handle(dev)
+    copy = lambda: _lib.check(lib.mc_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, h),  # noqa: E731
+                              "mc_stream_copy")
+    for _ in range(2):
+        copy()
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t0.record(stream)
     for _ in range(iters):
-        dst.copy_(src)
+        copy()
     t1.record(stream)
     torch.cuda.synchronize(dev)
     ms = t0.elapsed_time(t1) / iters
+    if not torch.equal(src[:1 << 20], dst[:1 << 20]):
+        raise RuntimeError("mc_stream_copy: copy mismatch")
     del src, dst
     torch.cuda.empty_cache()
     return 2 * nbytes / (ms * 1e-3) / 1e9
@@ -206,10 +216,25 @@ def _pmc_traffic():
     return (int(d["hbm_bytes"]) if d.get("hbm_bytes") else None), os.path.relpath(files[-1], ROOT)
 
 
+def _cpu_threads(args):
+    """Host threads for the CPU baseline: --cpu-threads, else every CPU this process may run on
+    (sched_getaffinity; os.cpu_count() when affinity is unavailable).  A GPU box that declares a
+    smaller CPU share through OMP_NUM_THREADS gets that share (more threads than cores only
+    oversubscribes them)."""
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(share)) if share.isdigit() and int(share) > 0 else n
+
+
 def cpu_baseline(args, model_name):
     import torch
     from oracle.cpu_model import cpu_train_pairs_per_sec
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    threads = _cpu_threads(args)
     prev = torch.get_num_threads()
     pps, secs = cpu_train_pairs_per_sec(model_name, batch=args.cpu_batch, steps=args.cpu_steps, warmup=1,
                                         threads=threads)
@@ -224,7 +249,7 @@ def cpu_baseline_scan(args):
     (model.py:83-169) on one C4 sequence batch (B=1 of 64, D=3072, L=4096, N=16, bf16 I/O)."""
     import torch
     from oracle.cpu_model import cpu_scan_gbps
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    threads = _cpu_threads(args)
     prev = torch.get_num_threads()
     gbs, secs = cpu_scan_gbps(batch=1, dim=3072, seqlen=4096, dstate=16, threads=threads)
     torch.set_num_threads(prev)

@@ -110,6 +110,11 @@ typedef struct mc_qkv_pack_params {
 } mc_qkv_pack_params;
 int mc_qkv_grad_pack(const mc_qkv_pack_params* p, void* stream);
 
+/* mc_stream_copy: dst[0, nbytes) = src[0, nbytes) with 16-B non-temporal vector loads / stores.
+ * A measurement utility with no reference counterpart: bench.py times it as the achievable
+ * HBM streaming rate next to the 8 TB/s spec.  16-B aligned, nbytes % 16 == 0. */
+int mc_stream_copy(const void* src, void* dst, size_t nbytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

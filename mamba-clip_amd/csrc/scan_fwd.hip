@@ -33,7 +33,7 @@ namespace scan {
 
 // FwdArgs: scan_common.h
 bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes);   // scan_fwd_pair.hip
-int launch_fwd_pair(const FwdArgs& a, int itype, int variant, hipStream_t s);
+int launch_fwd_pair(const FwdArgs& a, int itype, hipStream_t s);
 
 
 // Variants (template knobs, chosen on the host):
@@ -683,30 +683,11 @@ static int launch_fwd_v(const FwdArgs& a, bool aligned, hipStream_t s) {
 // vector-load B/C rings spill at the occupancy they need.  With short
 // sequences the grid is many short-lived waves and the SGPR-fed kernel wins;
 // with long ones the LDS-staged kernel's deeper prefetch wins.
-// MC_SCAN_FWD_VARIANT overrides the choice for A/B runs: 0 = LDS-staged (3 w/SIMD), 2 = LDS-staged
-// (2 w/SIMD), 10 = SGPR R=1, 8 = SGPR R=3.
-static int fwd_variant() {
-  static const int v = [] {
-    const char* e = getenv("MC_SCAN_FWD_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
+// A/B variants of this choice are built under tools/ (git history has the rejected kernels).
 template <typename TI, int kN>
 static int launch_fwd_n(const FwdArgs& a, bool aligned, hipStream_t s) {
-  int v = fwd_variant();
-  if (v < 0) v = a.seqlen <= 512 ? 10 : 0;
-  switch (v) {
-    case 8: return launch_fwd_mc<TI, kN, 3>(a, aligned, s);
-    case 10: return launch_fwd_mc<TI, kN, 1>(a, aligned, s);
-    case 2: return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
-    case 3: if (aligned && a.seqlen % kT == 0) return launch_fwd_v<TI, kN, 4, true, true, 3>(a, aligned, s);
-            return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
-    case 4: if (aligned && a.seqlen % kT == 0) return launch_fwd_v<TI, kN, 2, false, true, 3>(a, aligned, s);
-            return launch_fwd_v<TI, kN, 4, true, true, 2>(a, aligned, s);
-    default: return launch_fwd_v<TI, kN, 4, true, true, sizeof(TI) == 4 ? 1 : 2>(a, aligned, s);   // fp32: see launch_fwd_dirs
-  }
+  if (a.seqlen <= 512) return launch_fwd_mc<TI, kN, 1>(a, aligned, s);
+  return launch_fwd_v<TI, kN, 4, true, true, sizeof(TI) == 4 ? 1 : 2>(a, aligned, s);   // fp32: see launch_fwd_dirs
 }
 
 template <typename TI>
@@ -823,12 +804,9 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
     if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
     return launch_fwd_dirs<f16_t>(a, al, s);
   }
-  {   // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
-      // forward 0.166 vs 0.183 ms per layer); 20-23 force it (variants: scan_fwd_pair.hip)
-    const int v = fwd_variant();
-    if (fwd_pair_ok(a, aligned, ib) && (v < 0 || (v >= 20 && v <= 23)))
-      return launch_fwd_pair(a, p->itype, v, s);
-  }
+  // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
+  // forward 0.166 vs 0.183 ms per layer)
+  if (fwd_pair_ok(a, aligned, ib)) return launch_fwd_pair(a, p->itype, s);
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
   return launch_fwd_t<f16_t>(a, aligned, s);

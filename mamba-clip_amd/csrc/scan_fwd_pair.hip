@@ -34,19 +34,7 @@ constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
 
 // Packed (two positions) softplus and silu: the arithmetic around the transcendental
-// ops runs as v_pk_* (one issue for two positions).  Both softplus forms keep torch's
-// threshold (x > 20 -> x) without selects; softplus2_log1p is the default (variant 23),
-// softplus2 (one median) the A/B variant 20.
-__device__ __forceinline__ f32x2 softplus2(f32x2 x) {
-  const f32x2 arg = f32x2{fminf(x.x, 20.f), fminf(x.y, 20.f)} * kLog2e;
-  const f32x2 t = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
-  const f32x2 tp = t + 1.f;
-  const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)} * kLn2;
-  // x < lg < t holds for every x <= 20 (log1p(t) < t, log1p(e^x) > x), so the median is
-  // lg there; above 20 (t clamped to e^20, lg ~ 20) it is x: torch's threshold.  For
-  // x < -9 it is min(lg, t): lg can lose ~1e-7 absolute to the rounding of 1 + t.
-  return f32x2{__builtin_amdgcn_fmed3f(x.x, lg.x, t.x), __builtin_amdgcn_fmed3f(x.y, lg.y, t.y)};
-}
+// ops runs as v_pk_* (one issue for two positions).
 __device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
   // softplus(x) = max(x, 0) + log1p(exp(-|x|)): exp never overflows, and above 20 the log1p
   // term is below half an ulp of x, which is torch's threshold (x > 20 -> x) exactly.
@@ -90,7 +78,7 @@ struct PairLayout {
   static constexpr int kBCBytes = kT * 2 * kPN * 4;
 };
 
-template <typename TI, bool kSP, int kMinW, int kVar>
+template <typename TI, bool kSP, int kMinW>
 __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
   using PL = PairLayout<TI>;
   constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
@@ -184,9 +172,12 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
 #pragma unroll
         for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
           const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
-          f32x2 dt = kSP ? (kVar >= 1 ? softplus2_log1p(dr) : softplus2(dr)) : dr;
-          if constexpr (decltype(masked)::value) dt = vok ? dt : f32x2{0.f, 0.f};
-          const f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
+          f32x2 dt = kSP ? softplus2_log1p(dr) : dr;
+          f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
+          if constexpr (decltype(masked)::value) {   // u past L may be anything (stride padding): mask du too
+            dt = vok ? dt : f32x2{0.f, 0.f};
+            du = vok ? du : f32x2{0.f, 0.f};
+          }
           reinterpret_cast<float4*>(dst)[q] = make_float4(dt.x, dt.y, du.x, du.y);
         }
       }
@@ -219,12 +210,9 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           nq0 = *reinterpret_cast<const f32x4*>(row + tn * 8);
           nq1 = *reinterpret_cast<const f32x4*>(row + tn * 8 + 16);
         }
-        const float dtv[kPG] = {q0.x, q0.y, q1.x, q1.y};
-        const float duv[kPG] = {q0.z, q0.w, q1.z, q1.w};
         float yv[kPG];
 #pragma unroll
         for (int e = 0; e < kPG; ++e) {
-          const float dt = dtv[e], du = duv[e];
           const f32x4 b0 = nb0, b1 = nb1, c0v = nc0, c1v = nc1;
           {
             const f32x4* np = bcp + ((t0 + e + 1) & (kT - 1)) * (2 * kPN / 4);
@@ -234,15 +222,12 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           f32x2 dA[kPH / 2];
 #pragma unroll
           for (int p = 0; p < kPH / 2; ++p) {
-            f32x2 arg;
-            if constexpr (kVar >= 2)   // dt broadcast from its half of the {dt, dt} register pair
-              arg = (e & 1) ? pk_mul_bcast<1>(A2[p], e < 2 ? q0.xy : q1.xy)
-                            : pk_mul_bcast<0>(A2[p], e < 2 ? q0.xy : q1.xy);
-            else
-              arg = A2[p] * dt;                                             // v_pk_mul_f32
+            // dt broadcast from its half of the {dt, dt} register pair
+            const f32x2 arg = (e & 1) ? pk_mul_bcast<1>(A2[p], e < 2 ? q0.xy : q1.xy)
+                                      : pk_mul_bcast<0>(A2[p], e < 2 ? q0.xy : q1.xy);
             dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
           }
-          if constexpr (kVar >= 2) {   // du broadcast from its half of {du, du}
+          {   // du broadcast from its half of {du, du}
             const f32x2 dup = e < 2 ? q0.zw : q1.zw;
             if (e & 1) {
               x[0] = pk_fma_bcast<1>(b0.lo, dup, dA[0] * x[0]);
@@ -255,11 +240,6 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
               x[2] = pk_fma_bcast<0>(b1.lo, dup, dA[2] * x[2]);
               x[3] = pk_fma_bcast<0>(b1.hi, dup, dA[3] * x[3]);
             }
-          } else {
-            x[0] = dA[0] * x[0] + b0.lo * du;                                // v_pk_mul + v_pk_fma
-            x[1] = dA[1] * x[1] + b0.hi * du;
-            x[2] = dA[2] * x[2] + b1.lo * du;
-            x[3] = dA[3] * x[3] + b1.hi * du;
           }
           f32x2 y2 = c0v.lo * x[0];
           y2 = c0v.hi * x[1] + y2;
@@ -331,7 +311,7 @@ bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes) {
          fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) && (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds));
 }
 
-template <typename TI, int kMinW, int kVar>
+template <typename TI, int kMinW>
 static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   FwdArgs a = a0;
   const int H = a.dim / a.n_groups;
@@ -339,26 +319,21 @@ static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   a.total_blocks = a.batch * a.n_groups * a.nblk;
   const size_t lds = (size_t)PairLayout<TI>::kRowBytes + PairLayout<TI>::kBCBytes;
   if (a.softplus)
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, kVar>), dim3(a.total_blocks), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
   else
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, kVar>), dim3(a.total_blocks), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }
 
 // 16-bit rows only (fp32 rows double the staging registers and spill at 3 waves / SIMD).
-// variant (A/B builds, MC_SCAN_FWD_VARIANT; interleaved on one box, tools/ab_pair_variants.sh, C4 ms):
-// 20 median softplus 2.82, 21 = 20 at 4 waves/SIMD (spills) 3.59, 22 log1p softplus 2.80,
-// 23 (default) = 22 + op_sel broadcasts of dt / du in inline asm 2.78; one-channel kernel 3.26
-int launch_fwd_pair(const FwdArgs& a, int itype, int variant, hipStream_t s) {
-  if (itype == MC_DTYPE_BF16) {
-    if (variant == 21) return launch_pair_t<bf16_t, 4, 0>(a, s);
-    if (variant == 20) return launch_pair_t<bf16_t, 3, 0>(a, s);
-    if (variant == 22) return launch_pair_t<bf16_t, 3, 1>(a, s);
-    return launch_pair_t<bf16_t, 3, 2>(a, s);
-  }
-  return launch_pair_t<f16_t, 3, 2>(a, s);
+// Measured alternatives (interleaved on one box, C4 ms; built under tools/ for A/B runs):
+// median softplus 2.82, the same at 4 waves/SIMD (spills) 3.59, log1p softplus 2.80,
+// + op_sel broadcasts of dt / du in inline asm (this kernel) 2.78; one-channel kernel 3.26.
+int launch_fwd_pair(const FwdArgs& a, int itype, hipStream_t s) {
+  if (itype == MC_DTYPE_BF16) return launch_pair_t<bf16_t, 3>(a, s);
+  return launch_pair_t<f16_t, 3>(a, s);
 }
 
 }  // namespace scan

@@ -138,6 +138,7 @@ SYMBOLS = {
     "mc_gelu_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_fp, c_vp,
                                    ctypes.c_size_t, c_vp]),
     "mc_qkv_grad_pack": (ctypes.c_int, [ctypes.POINTER(QkvPackParams), c_vp]),
+    "mc_stream_copy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, c_vp]),
 }
 
 _lib = None

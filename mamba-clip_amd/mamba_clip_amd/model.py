@@ -308,9 +308,12 @@ class BertTextEncoder(nn.Module):
 
 # ============================================================================ CLIP wrapper (model.py:998-1112)
 def _is_norm_param(name):
-    """Our towers' LayerNorm / RMSNorm parameters (the HF towers' "LayerNorm" modules)."""
-    leaf = name.split(".")
-    return any(part in ("ln", "norm1", "norm2", "norm_weight", "norm_f") for part in leaf)
+    """Parameters of the modules the reference's lock_text_tower keeps under `freeze_layer_norm`:
+    those under a module literally named "LayerNorm" (model.py:1076, 1094-1096), i.e. HF BERT's
+    embedding / attention-output / output LayerNorms = our BERT tower's ln / norm1 / norm2.  The
+    Mamba LM's RMSNorms (HF names norm / norm_f) match no "LayerNorm" and are frozen with the rest."""
+    return any(part in ("ln", "norm1", "norm2") for part in name.split("."))
+
 
 class ClipModel(nn.Module):
     """ClipModel(model) as the reference (model.py:1001-1009): wraps a CLIP-like model and SHARES its
@@ -666,9 +669,9 @@ class VSSM(nn.Module):
 
 # ============================================================================ factory (model.py:1257-1289)
 MODEL_CONFIGS = {
-    # C1: tiny plumbing config (BASELINE configs[0])
+    # C1: tiny plumbing config (BASELINE configs[0]): Mamba text d_model 128, L = 256, d_state 16, 32-dim output
     "tiny-mamba-clip": dict(vision=dict(img_size=32, patch=8, width=64, layers=2, heads=4, output_dim=32),
-                            text=dict(vocab_size=1000, context_length=16, d_model=128, n_layer=2, output_dim=32)),
+                            text=dict(vocab_size=1000, context_length=256, d_model=128, n_layer=2, output_dim=32)),
     # C2: ViT-B/16 + Mamba-130M text (BASELINE configs[1])
     "vit_b16-mamba130m": dict(vision=dict(), text=dict(vocab_size=50280, context_length=77, d_model=768,
                                                         n_layer=24, output_dim=512)),

@@ -196,16 +196,11 @@ def ce_fused_grad(X, Y, sc, lse_r, lse_c, row_off, coef_r, col_off, coef_c, gout
 
 
 def _mm(a, b, out):
-    """torch.mm; fp32 operands at exact fp32 (gfx950 has full-rate-for-f32 MFMA), even when the
-    process enabled TF32-class matmuls (init_device sets allow_tf32 like the reference CLI)."""
-    if a.dtype != torch.float32:
-        return torch.mm(a, b, out=out)
-    prev = torch.backends.cuda.matmul.allow_tf32
-    torch.backends.cuda.matmul.allow_tf32 = False
-    try:
-        return torch.mm(a, b, out=out)
-    finally:
-        torch.backends.cuda.matmul.allow_tf32 = prev
+    """torch.mm into ``out``.  fp32 operands run the library's fp32 GEMM: gfx950 has no reduced-
+    precision (xf32) matrix path, so the process-wide allow_tf32 flag (set by init_device like the
+    reference, utils/dist_utils.py:41-43) does not change these products; tests/test_loss_gpu.py
+    checks that on the box.  No global state is touched here (thread-safe)."""
+    return torch.mm(a, b, out=out)
 
 
 def _block_rows(other):
@@ -664,6 +659,14 @@ def _aligned_rows(t, V):
     return t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and t.stride(0) % V == 0
 
 
+def _hip_rows(t, V, who):
+    """t with 16-B aligned rows for a HIP kernel: a fresh dense copy when t's layout does not
+    qualify.  There is no torch fallback on the GPU: a width the kernel cannot tile raises."""
+    if t.shape[-1] % V:
+        raise RuntimeError(f"{who}: row width {t.shape[-1]} must be a multiple of {V} elements")
+    return t if _aligned_rows(t, V) else t.clone(memory_format=torch.contiguous_format)
+
+
 class FC1GeluFn(torch.autograd.Function):
     """a = gelu(x @ w^T + b) -- the MLP's first projection and activation (timm Mlp fc1 + GELU).
 
@@ -688,8 +691,9 @@ class FC1GeluFn(torch.autograd.Function):
         h2 = h.reshape(-1, cols)
         g2 = ga.reshape(-1, cols).to(h.dtype)
         V = 16 // h.element_size()
-        if h.is_cuda and cols % V == 0 and _aligned_rows(h2, V) and _aligned_rows(g2, V):
+        if h.is_cuda:
             lib = _lib.load()
+            h2, g2 = _hip_rows(h2, V, "fc1_gelu backward"), _hip_rows(g2, V, "fc1_gelu backward")
             gh = torch.empty_like(h2)
             db = torch.empty(cols, device=h.device, dtype=torch.float32)
             ws_b = lib.mc_grad_colsum_workspace_bytes(h2.shape[0], cols)
@@ -697,7 +701,7 @@ class FC1GeluFn(torch.autograd.Function):
             _lib.check(lib.mc_gelu_bwd(h2.shape[0], cols, _lib.dtype_code(h.dtype), h2.data_ptr(), h2.stride(0),
                                        g2.data_ptr(), g2.stride(0), gh.data_ptr(), gh.stride(0), db.data_ptr(),
                                        ws.data_ptr(), ws_b, _lib.stream_handle(h.device)), "mc_gelu_bwd")
-        else:
+        else:   # CPU tensors (the CPU restatement tests): the same math in torch
             gh = torch.ops.aten.gelu_backward(g2, h2)
             db = gh.sum(0, dtype=torch.float32)
         x2 = xc.reshape(-1, xc.shape[-1])
@@ -739,9 +743,11 @@ class QKVProjFn(torch.autograd.Function):
                  for g in (dq, dk, dv)]
         grads = [g.to(xc.dtype) for g in grads]
         V = 16 // xc.element_size()
-        ok = xc.is_cuda and D % V == 0 and all(
-            g.stride(-1) == 1 and g.data_ptr() % 16 == 0 and all(st % V == 0 for st in g.stride()[:3]) for g in grads)
-        if ok:
+        if xc.is_cuda:
+            if D % V:
+                raise RuntimeError(f"qkv_proj backward: head_dim {D} must be a multiple of {V}")
+            grads = [g if (g.stride(-1) == 1 and g.data_ptr() % 16 == 0 and all(st % V == 0 for st in g.stride()[:3]))
+                     else g.contiguous() if not g.is_contiguous() else g.clone() for g in grads]
             lib = _lib.load()
             g2 = torch.empty(Bsz * N, 3 * C, device=xc.device, dtype=xc.dtype)
             db = torch.empty(3 * C, device=xc.device, dtype=torch.float32)
@@ -755,7 +761,7 @@ class QKVProjFn(torch.autograd.Function):
             p.out, p.ld_out, p.dbias = g2.data_ptr(), 3 * C, db.data_ptr()
             p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
             _lib.check(lib.mc_qkv_grad_pack(p, _lib.stream_handle(xc.device)), "mc_qkv_grad_pack")
-        else:
+        else:   # CPU tensors (the CPU restatement tests): the same math in torch
             g2 = torch.stack([g.transpose(1, 2) for g in grads], dim=2).reshape(Bsz * N, 3 * C)
             db = g2.sum(0, dtype=torch.float32)
         dx = torch.mm(g2, wc).view(xc.shape) if ctx.needs_input_grad[0] else None

@@ -227,6 +227,9 @@ class GroupedScanFn(torch.autograd.Function):
         bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
         batch, dim, L = delta.shape
         G = B.shape[1]
+        if not (1 <= u_groups <= G and G % u_groups == 0):
+            # the backward sums the G / u_groups groups sharing a u block (du.view(b, G // k, k, ...))
+            raise RuntimeError(f"grouped_scan_fn: u_groups={u_groups} must divide n_groups={G}")
         if (dim % G or u.shape != (batch, u_groups * (dim // G), L) or B.shape[0] != batch
                 or B.shape[3] != L or C.shape != B.shape):
             raise RuntimeError("grouped_scan_fn: u (B, u_groups*dim/G, L), delta (B, dim, L), B/C (B, G, N, L) expected")

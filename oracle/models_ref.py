@@ -39,8 +39,9 @@ def causal_conv1d_ref(x, w, b, silu=True):
 
 
 def mamba_mixer_ref(m, hidden):
-    """mixer math in fp64 with the module's parameters (m: MambaMixer)."""
-    p = {k: v.detach().double().cpu() for k, v in m.state_dict().items()}
+    """mixer math in fp64 with the module's parameters (m: MambaMixer), on hidden's device (the same
+    torch code on the host or, for full-size checks, evaluated on the GPU in fp64)."""
+    p = {k: v.detach().to(hidden.device, torch.float64) for k, v in m.state_dict().items()}
     h = hidden.double()
     xz = torch.einsum("ed,bld->bel", p["in_proj.weight"], h)
     x, z = xz[:, : m.d_inner], xz[:, m.d_inner:]

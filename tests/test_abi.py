@@ -38,7 +38,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mamba_clip_amd import _lib
     lib = _lib.load()
-    C = _lib.MC_SCAN_CHUNK          # saved-state granularity (8 positions)
+    C = _lib.MC_SCAN_CHUNK          # saved-state granularity (32 positions, include/mc_scan.h)
     assert lib.mc_scan_n_chunks(0) == 0
     assert lib.mc_scan_n_chunks(1) == 1
     assert lib.mc_scan_n_chunks(C) == 1

@@ -1,0 +1,252 @@
+"""One driver-runnable GPU test per BASELINE.json config, at the config's own shape.
+
+  C1  tiny Mamba text (d_model 128, L 256, d_state 16, 32-dim output), batch 8, via the
+      mamba-clip CLI, plus one fwd + bwd against the CPU restatement (oracle_ops) at that shape
+  C2  ViT-B/16 + Mamba-130M, batch 256, amp_bf16: product train_step; one Mamba-130M mixer at
+      the C2 channel-major shape (256 x 1536 x 80) fwd + every gradient vs the fp64 oracle
+  C3  BiomedCLIP ViT-B/16 + PubMedBERT-256 at batch 64: tests/test_model_gpu.py
+      (test_biomedclip_c3_full_size_trains_on_one_gpu, test_bert_clip_tiny_matches_cpu_restatement)
+  C4  the scan backward at the C4 sequence shape (D 3072, L 4096, N 16, bf16, z) vs the fp64 oracle:
+      per-channel gradients on channel slices (host oracle), dB / dC over all 3072 channels
+      (the same fp64 oracle code evaluated on the device); one Mamba-790M mixer layer at C4
+      (batch 64, L 4096, d_model 1536) fwd + bwd, batch rows vs the fp64 oracle
+  C5  fp8 similarity at N = 8192: tests/test_fp8_gpu.py
+
+Reference semantics: scan model.py:83-169 (call site 539-550), ClipLoss loss.py:56-147, train step
+train.py:92-385.  The fp64 oracle (oracle/) is the checker; the product path never touches it.
+"""
+import json
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+import oracle.models_ref as R
+from oracle.scan_ref import selective_scan_ref, selective_scan_ref_grads
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(got, want):
+    got, want = got.detach().double(), want.detach().double().to(got.device)
+    return float((got - want).abs().max()) / max(float(want.abs().max()), 1e-30)
+
+
+# ----------------------------------------------------------------------------------------------- C1
+def test_c1_cli_tiny_mamba_l256(capsys):
+    """BASELINE configs[0] through the CLI: tiny-mamba-clip's text tower is d_model 128, L 256,
+    d_state 16, 32-dim output; batch 8."""
+    from mamba_clip_amd.cli import main
+    from mamba_clip_amd.model import MODEL_CONFIGS
+    t = MODEL_CONFIGS["tiny-mamba-clip"]["text"]
+    assert (t["d_model"], t["context_length"], t["output_dim"]) == (128, 256, 32)
+    rc = main(["--synthetic", "--model", "tiny-mamba-clip", "--batch-size", "8", "--train-num-samples", "24",
+               "--benchmark", "--log-every-n-steps", "1", "--precision", "amp_bf16"])
+    assert rc == 0
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["pairs_per_sec"] > 0 and out["final"]["loss"] is not None
+
+
+def test_c1_shape_matches_cpu_restatement():
+    """C1 fwd + ClipLoss + bwd on cuda (HIP scan / conv / norms at L 256) vs the same weights on the
+    CPU restatement (oracle_ops: the scan is the reference-semantics loop)."""
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import build_clip
+    from oracle.cpu_model import oracle_clip_loss, oracle_ops
+    torch.manual_seed(11)
+    cpu = build_clip("tiny-mamba-clip")
+    gpu = build_clip("tiny-mamba-clip")
+    gpu.load_state_dict(cpu.state_dict())
+    gpu = gpu.to(DEV)
+    g = torch.Generator().manual_seed(12)
+    img = torch.randn(8, 3, 32, 32, generator=g)
+    tok = torch.randint(1, 999, (8, 256), generator=g)
+    tok[:, -1] = 999
+    out = gpu(img.to(DEV), tok.to(DEV))
+    loss = ClipLoss()(**out)["contrastive_loss"]
+    loss.backward()
+    with oracle_ops():
+        ref = cpu(img, tok)
+        ref_loss = oracle_clip_loss(**ref)["contrastive_loss"]
+        ref_loss.backward()
+    assert _rel(out["text_features"], ref["text_features"]) < 1e-4
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    rp = dict(cpu.named_parameters())
+    for n, p in gpu.named_parameters():
+        if p.grad is not None:
+            assert _rel(p.grad, rp[n].grad) < 5e-3, n
+
+
+# ----------------------------------------------------------------------------------------------- C2
+def test_c2_full_size_train_steps():
+    """BASELINE configs[1]: ViT-B/16 + Mamba-130M at batch 256, 77-token text, amp_bf16; the
+    product train_step (fwd, ClipLoss, bwd, fused AdamW, clamp).  Tower arithmetic vs open_clip is
+    unpinned (absent offline), so the full size is checked by properties: finite, decreasing loss
+    on a fixed batch; unit-norm features; logit_scale clamped to [0, ln 100]."""
+    import math
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import build_clip
+    from mamba_clip_amd.train import create_optimizer, train_step
+    torch.manual_seed(0)
+    model = build_clip("vit_b16-mamba130m").to(DEV)
+    assert model.context_length == 77 and len(model.text.layers) == 24 and model.text.layers[0].mixer.d_inner == 1536
+    args = SimpleNamespace(precision="amp_bf16", lr=1e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
+                           grad_clip_norm=None)
+    opt = create_optimizer(model, args)
+    images, texts, targets = synthetic_batch(256, 224, 77, model.vocab_size, device=DEV, seed=1000)
+    losses = [float(train_step(model, images, texts, targets, ClipLoss(), opt, None, args)["loss"])
+              for _ in range(3)]
+    assert all(math.isfinite(x) for x in losses) and losses[-1] < losses[0], losses
+    assert 0.0 <= float(model.logit_scale) <= math.log(100) + 1e-6
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model(images, texts)
+    for k in ("image_features", "text_features"):
+        assert out[k].shape == (256, 512) and torch.isfinite(out[k]).all()
+        torch.testing.assert_close(out[k].float().norm(dim=-1), torch.ones(256, device=DEV), rtol=0, atol=1e-2)
+
+
+def test_c2_mamba130m_mixer_full_shape_vs_fp64():
+    """One Mamba-130M mixer (d_model 768, d_inner 1536, dt_rank 48, d_state 16) at the C2 text shape
+    (batch 256, 77 tokens padded to 80: the scan sees 256 x 1536 x 80 channel-major) in fp32: output
+    and the input / every parameter gradient vs the fp64 oracle (oracle/models_ref.mamba_mixer_ref,
+    evaluated on the device in fp64 so the full batch fits the time budget)."""
+    from mamba_clip_amd.model import MambaMixer
+    torch.manual_seed(21)
+    m = MambaMixer(768, d_state=16).to(DEV)
+    assert (m.d_inner, m.dt_rank) == (1536, 48)
+    h = torch.randn(256, 80, 768, device=DEV, requires_grad=True)
+    gy = torch.randn(256, 80, 768, device=DEV)
+    out = m(h)
+    out.backward(gy)
+    hr = h.detach().double().requires_grad_(True)
+    mr = {k: v.detach().double().requires_grad_(True) for k, v in m.named_parameters()}
+    ref = _mixer_ref_params(m, mr, hr)
+    ref.backward(gy.double())
+    assert _rel(out, ref) < 1e-4
+    assert _rel(h.grad, hr.grad) < 1e-3
+    for n, p in m.named_parameters():
+        assert _rel(p.grad, mr[n].grad) < 2e-3, n
+
+
+def test_c2_mamba130m_mixer_bf16_autocast_vs_fp64():
+    """The same mixer under amp_bf16 (the C2 path: bf16 channel-major activations, the pair scan
+    kernels): output and input gradient within bf16-level error of the fp64 oracle."""
+    from mamba_clip_amd.model import MambaMixer
+    torch.manual_seed(22)
+    m = MambaMixer(768, d_state=16).to(DEV)
+    h = torch.randn(256, 80, 768, device=DEV).bfloat16().float().requires_grad_(True)
+    gy = torch.randn(256, 80, 768, device=DEV).bfloat16().float()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(h)
+    out.float().backward(gy)
+    hr = h.detach().double().requires_grad_(True)
+    ref = R.mamba_mixer_ref(m, hr)
+    ref.backward(gy.double())
+    assert _rel(out.float(), ref) < 3e-2
+    assert _rel(h.grad, hr.grad) < 5e-2
+
+
+def _mixer_ref_params(m, p, h):
+    """mamba_mixer_ref with differentiable fp64 parameters p (name -> leaf)."""
+    import torch.nn.functional as F
+    xz = torch.einsum("ed,bld->bel", p["in_proj.weight"], h)
+    x, z = xz[:, : m.d_inner], xz[:, m.d_inner:]
+    D, K = p["conv1d.weight"].shape[0], p["conv1d.weight"].shape[-1]
+    x = F.silu(F.conv1d(x, p["conv1d.weight"].reshape(D, 1, K), p["conv1d.bias"], padding=K - 1,
+                        groups=D)[..., : x.shape[-1]])
+    x_dbl = torch.einsum("cd,bdl->bcl", p["x_proj.weight"], x)
+    dt_raw, Bm, Cm = torch.split(x_dbl, [m.dt_rank, m.d_state, m.d_state], dim=1)
+    delta = torch.einsum("dr,brl->bdl", p["dt_proj.weight"], dt_raw)
+    y = selective_scan_ref(x, delta, -torch.exp(p["A_log"]), Bm, Cm, p["D"], z=z, delta_bias=p["dt_proj.bias"],
+                           delta_softplus=True, compute_dtype=torch.float64)
+    return torch.einsum("md,bdl->blm", p["out_proj.weight"], y)
+
+
+# ----------------------------------------------------------------------------------------------- C4
+GRAD_REL_BF16 = 2.0 ** -7
+
+
+def _assert_grad(got, want, what, rel=GRAD_REL_BF16):
+    got, want = got.detach().double(), want.detach().double().to(got.device)
+    tol = 2e-4 * float(want.abs().max()) + rel * want.abs()
+    bad = (got - want).abs() > tol
+    assert not bad.any(), (f"{what}: {int(bad.sum())}/{bad.numel()} outside tolerance, max abs err "
+                           f"{float((got - want).abs().max()):.3e} (max |ref| {float(want.abs().max()):.3e})")
+
+
+def _c4_case(Bsz, D=3072, L=4096, N=16, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    bf = torch.bfloat16
+    x = dict(u=torch.randn(Bsz, D, L, device=DEV, generator=g).to(bf),
+             delta=(0.5 * torch.randn(Bsz, D, L, device=DEV, generator=g)).to(bf),
+             A=-torch.exp(torch.log(torch.arange(1, N + 1, dtype=torch.float32, device=DEV)).repeat(D, 1)
+                          + 0.1 * torch.randn(D, N, device=DEV, generator=g)),
+             B=torch.randn(Bsz, 1, N, L, device=DEV, generator=g).to(bf),
+             C=torch.randn(Bsz, 1, N, L, device=DEV, generator=g).to(bf),
+             D=torch.randn(D, device=DEV, generator=g),
+             z=torch.randn(Bsz, D, L, device=DEV, generator=g).to(bf),
+             delta_bias=torch.rand(D, device=DEV, generator=g) * 4 - 5)
+    dout = torch.randn(Bsz, D, L, device=DEV, generator=g).to(bf)
+    return x, dout
+
+
+def test_c4_scan_backward_full_shape_vs_fp64():
+    """Scan backward at the C4 sequence shape (batch 2 of 64, D 3072, L 4096 = 128 saved-state
+    chunks, N 16, bf16 u / delta / z / B / C, softplus, D, bias).
+      * du, ddelta, dz, dA, dD, dbias of channels 0..63 and 3008..3071 vs the host fp64 oracle
+        (those gradients of a channel depend only on that channel's rows);
+      * dB, dC (sums over all 3072 channels) and every other gradient vs the same fp64 oracle code
+        evaluated on the device over the whole problem."""
+    from mamba_clip_amd.selective_scan_interface import selective_scan_fn
+    x, dout = _c4_case(2)
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in x.items()}
+    out = selective_scan_fn(**leaves, delta_softplus=True)
+    out.backward(dout)
+    torch.cuda.synchronize()
+    for d0 in (0, 3008):
+        sl = slice(d0, d0 + 64)
+        xs = {k: (v[:, sl] if k in ("u", "delta", "z") else v[sl] if k in ("A", "D", "delta_bias") else v).cpu()
+              for k, v in x.items()}
+        ref = selective_scan_ref_grads(**xs, delta_softplus=True, dout=dout[:, sl].cpu().double(),
+                                       compute_dtype=torch.float64)
+        for k in ("u", "delta", "z"):
+            _assert_grad(leaves[k].grad[:, sl], ref[k], f"d{k}[{d0}:]")
+        for k in ("A", "D", "delta_bias"):
+            _assert_grad(leaves[k].grad[sl], ref[k], f"d{k}[{d0}:]", rel=1e-4)
+    full = selective_scan_ref_grads(**x, delta_softplus=True, dout=dout.double(), compute_dtype=torch.float64)
+    for k in ("B", "C", "u", "delta", "z"):
+        _assert_grad(leaves[k].grad, full[k], f"d{k} (all channels)")
+    for k in ("A", "D", "delta_bias"):
+        _assert_grad(leaves[k].grad, full[k], f"d{k} (all channels)", rel=1e-4)
+
+
+def test_c4_mamba790m_layer_fwd_bwd():
+    """One Mamba-790M layer (add + RMSNorm, mixer d_model 1536 / d_inner 3072 / dt_rank 96) at the C4
+    shape: batch 64, L 4096, amp_bf16, fwd + bwd.  Every output and gradient finite; batch rows 0 and
+    63 (a layer is independent per batch row) within bf16-level error of the fp64 oracle."""
+    from mamba_clip_amd.model import MODEL_CONFIGS, MambaLayer
+    t = MODEL_CONFIGS["mamba790m-text"]["text"]
+    assert (t["d_model"], t["context_length"], t["n_layer"]) == (1536, 4096, 48)
+    torch.manual_seed(31)
+    layer = MambaLayer(1536, d_state=16).to(DEV)
+    assert (layer.mixer.d_inner, layer.mixer.dt_rank) == (3072, 96)
+    g = torch.Generator(device=DEV).manual_seed(32)
+    hid = torch.randn(64, 4096, 1536, device=DEV, generator=g).bfloat16().requires_grad_(True)
+    gy = torch.randn(64, 4096, 1536, device=DEV, generator=g).bfloat16()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out, res = layer(hid, None)
+    out.backward(gy)
+    assert out.shape == (64, 4096, 1536) and torch.isfinite(out).all()
+    assert torch.isfinite(hid.grad).all()
+    for n, p in layer.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), n
+    for b in (0, 63):
+        hr = hid[b:b + 1].detach().double().requires_grad_(True)
+        normed = R.rmsnorm_ref(hr, None, layer.norm_weight.detach())[0]
+        ref = R.mamba_mixer_ref(layer.mixer, normed)
+        ref.backward(gy[b:b + 1].double())
+        assert _rel(out[b:b + 1].float(), ref) < 3e-2, b
+        assert _rel(hid.grad[b:b + 1].float(), hr.grad) < 5e-2, b

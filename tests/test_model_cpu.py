@@ -118,7 +118,7 @@ def test_clip_model_reference_constructor_shares_logit_params():
     wrapped = ClipModel(base)
     assert wrapped.visual is base.visual and wrapped.text is base.text
     assert wrapped.logit_scale is base.logit_scale and wrapped.logit_bias is base.logit_bias
-    assert wrapped.context_length == 16 and wrapped.vocab_size == 1000
+    assert wrapped.context_length == 256 and wrapped.vocab_size == 1000
 
     class Raw(nn.Module):                   # an open_clip-like CLIP that is not a ClipModel
         def __init__(self):
@@ -142,8 +142,9 @@ def test_lock_text_tower_freezes_embeddings_and_layers():
     m.lock_text_tower()
     assert trainable(m) == {"proj.weight"}
     m = build_clip("tiny-mamba-clip")
+    # the Mamba RMSNorms (HF norm / norm_f) are not "LayerNorm" modules: frozen either way (model.py:1076)
     m.lock_text_tower(freeze_layer_norm=False)
-    assert trainable(m) == {"proj.weight", "norm_f", "layers.0.norm_weight", "layers.1.norm_weight"}
+    assert trainable(m) == {"proj.weight"}
     m = build_clip("tiny-mamba-clip")
     m.lock_text_tower(unlocked_layers=1)
     t = trainable(m)
@@ -156,6 +157,11 @@ def test_lock_text_tower_freezes_embeddings_and_layers():
     t = trainable(bm)
     assert not {"tok.weight", "pos", "ln.weight"} & t and not any(n.startswith("blocks.0.") for n in t)
     assert any(n.startswith("blocks.1.") for n in t) and any(n.startswith("proj.") for n in t)
+    # BERT's LayerNorms (embeddings + both per block) follow `not freeze_layer_norm`
+    bm.lock_text_tower(freeze_layer_norm=False)
+    t = trainable(bm)
+    assert {"ln.weight", "ln.bias", "blocks.0.norm1.weight", "blocks.1.norm2.bias"} <= t
+    assert not any(("attn" in n or "fc" in n) for n in t) and "tok.weight" not in t
 
 
 def test_ss2d_parameter_inits_follow_reference_statistics():

@@ -547,3 +547,40 @@ def test_clip_classifier_head_on_frozen_features():
         torch.testing.assert_close(prob.sum(1).cpu(), torch.ones(8))
         assert torch.equal(pred.cpu(), ref.argmax(1))
         heads[str(variant)] = logits
+
+
+def test_glue_ops_take_the_hip_path_for_unaligned_views_and_raise_on_odd_widths():
+    """fc1_gelu / qkv_proj backward on the GPU run the HIP kernels (mc_gelu_bwd, mc_qkv_grad_pack)
+    for any layout -- an unaligned view is copied to aligned rows first, there is no ATen fallback --
+    and a width the kernels cannot tile raises instead of silently leaving the HIP path."""
+    from mamba_clip_amd import ops
+    torch.manual_seed(5)
+    w = torch.randn(64, 40, device=DEV, requires_grad=True)
+    bias = torch.randn(64, device=DEV, requires_grad=True)
+    base = torch.randn(7 * 41 + 1, device=DEV)
+    x = base[1:].view(7, 41)[:, :40].requires_grad_(False)     # unaligned rows (offset 4 B, stride 41)
+    calls = []
+    orig_load = ops._lib.load
+    lib = orig_load()
+
+    class Spy:
+        def __getattr__(self, n):
+            return getattr(lib, n)
+
+        def mc_gelu_bwd(self, *a):
+            calls.append(1)
+            return lib.mc_gelu_bwd(*a)
+    ops._lib.load = lambda: Spy()
+    M = torch.randn(64, 7, device=DEV)
+    try:   # the gradient reaching fc1_gelu is M.t(): a transposed (column-major) view
+        (ops.fc1_gelu(x, w, bias).t() * M).sum().backward()
+    finally:
+        ops._lib.load = orig_load
+    assert calls, "mc_gelu_bwd was not called"
+    xr, wr, br = x.double(), w.detach().double().requires_grad_(True), bias.detach().double().requires_grad_(True)
+    (torch.nn.functional.gelu(xr @ wr.T + br).t() * M.double()).sum().backward()
+    torch.testing.assert_close(w.grad.double(), wr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bias.grad.double(), br.grad, rtol=1e-4, atol=1e-4)
+    w3 = torch.randn(66, 40, device=DEV, requires_grad=True)         # 66 columns: not a multiple of 4
+    with pytest.raises(RuntimeError):
+        ops.fc1_gelu(x, w3, torch.zeros(66, device=DEV, requires_grad=True)).sum().backward()

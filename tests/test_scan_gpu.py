@@ -313,3 +313,26 @@ def test_grouped_scan_rejects_bad_configs():
     with pytest.raises(RuntimeError):   # mask beyond n_groups
         grouped_scan_fn(torch.randn(1, 16, 12, device=DEV), torch.randn(1, 32, 12, device=DEV), A, Bm, Bm,
                         reverse_groups=0b110000, u_groups=2)
+
+
+def test_scan_fwd_pair_masked_chunk_ignores_nan_padding():
+    """Pair kernel, L % 32 != 0: the last chunk reads u / delta past L (the row stride padding).
+    Those positions are masked (dt = du = 0), so NaN / Inf in the padding cannot reach the state:
+    out and last_state equal the result with zero padding (and the fp64 oracle)."""
+    selective_scan_fn = _lib_fn()
+    x = _rand_case(2, 64, 1000, 16, 1, torch.bfloat16, torch.bfloat16, seed=17)
+    views = {}
+    for k in ("u", "delta", "z"):
+        big = torch.full((2, 64, 1024), float("nan"), dtype=torch.bfloat16)
+        big[:, :, 1000:1008] = float("inf")
+        big[:, :, :1000] = x[k]
+        views[k] = big.to(DEV)[:, :, :1000]
+        assert views[k].stride(1) == 1024
+    rest = {k: v.to(DEV) for k, v in x.items() if k not in views}
+    out, last = selective_scan_fn(**views, **rest, delta_softplus=True, return_last_state=True)
+    dense = {k: v.to(DEV) for k, v in x.items()}
+    out0, last0 = selective_scan_fn(**dense, delta_softplus=True, return_last_state=True)
+    assert torch.isfinite(last).all() and torch.isfinite(out).all()
+    assert torch.equal(out, out0) and torch.equal(last, last0)
+    _, ref_last = selective_scan_ref(**x, delta_softplus=True, return_last_state=True, compute_dtype=torch.float64)
+    assert_scan_close(last, ref_last, torch.float32, "last_state")
