@@ -21,7 +21,7 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
-def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32, scale_a=None, scale_b=None):
+def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32, scale_a=None, scale_b=None, out=None):
     """C[m, n] = alpha * scale_a[m] * scale_b[n] * sum_k A[m, k] * B[n, k]  (A, B row-major, K contiguous).
 
     scale_a / scale_b (fp32 per-row factors, optional) are the dequantisation
@@ -38,11 +38,16 @@ def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32, scale_a=No
     N, K2 = B.shape
     if K != K2:
         raise RuntimeError("gemm_nt: inner dimensions differ")
-    C = torch.empty(M, N, device=A.device, dtype=out_dtype)
+    if out is None:
+        C = torch.empty(M, N, device=A.device, dtype=out_dtype)
+    else:
+        if out.shape != (M, N) or out.dtype != out_dtype or out.stride(-1) != 1:
+            raise RuntimeError("gemm_nt: out must be (M, N) of out_dtype with unit column stride")
+        C = out
     p = _lib.GemmNTParams()
     p.M, p.N, p.K = M, N, K
     p.in_dtype, p.out_dtype = _lib.dtype_code(A.dtype), _lib.dtype_code(out_dtype)
-    p.A, p.lda, p.B, p.ldb, p.C, p.ldc = A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), N
+    p.A, p.lda, p.B, p.ldb, p.C, p.ldc = A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0)
     p.alpha = float(alpha)
     p.alpha_dev = alpha_dev.data_ptr() if alpha_dev is not None else None
     for name, sc, n in (("row_scale_a", scale_a, M), ("row_scale_b", scale_b, N)):
@@ -195,12 +200,14 @@ def ce_fused_grad(X, Y, sc, lse_r, lse_c, row_off, coef_r, col_off, coef_c, gout
     return G, dscale
 
 
-def _mm(a, b, out):
-    """torch.mm into ``out``.  fp32 operands run the library's fp32 GEMM: gfx950 has no reduced-
-    precision (xf32) matrix path, so the process-wide allow_tf32 flag (set by init_device like the
-    reference, utils/dist_utils.py:41-43) does not change these products; tests/test_loss_gpu.py
-    checks that on the box.  No global state is touched here (thread-safe)."""
-    return torch.mm(a, b, out=out)
+def _mm_nt(a, b_t, out):
+    """out = a @ b_t^T.  fp32 operands run the library's exact-fp32 MFMA GEMM (mc_gemm_nt, b_t
+    K-contiguous): a library fp32 GEMM follows the process-wide allow_tf32 flag, which init_device
+    turns on like the reference (utils/dist_utils.py:41-43) -- flipping that flag here would race
+    with other threads.  bf16 operands run the library GEMM (no reduced-precision variant)."""
+    if a.dtype == torch.float32:
+        return gemm_nt(a, b_t, out=out)
+    return torch.mm(a, b_t.t(), out=out)
 
 
 def _block_rows(other):
@@ -245,6 +252,9 @@ class ScaledLogitsCE(torch.autograd.Function):
         M, N = Xc.shape[0], Yc.shape[0]
         want_ds = ctx.needs_input_grad[2]
         dX = dY = dscale = None
+        # second operands of dX = G @ Y and dY = G^T @ X as (K-contiguous) row-major transposes
+        Yt = Yc.t().contiguous() if Yc.dtype == torch.float32 else Yc.t()
+        Xt = Xc.t().contiguous() if Xc.dtype == torch.float32 else Xc.t()
         if ctx.needs_input_grad[0] or want_ds:
             dX = torch.empty_like(Xc) if ctx.needs_input_grad[0] else None
             R = _block_rows(N)
@@ -254,7 +264,7 @@ class ScaledLogitsCE(torch.autograd.Function):
                 G, ds = ce_fused_grad(Xc[r0:r1], Yc, sc, lse_r[r0:r1], lse_c, row_off + r0, coef_r, col_off - r0,
                                       coef_c, gout, gdt, want_ds)
                 if dX is not None:
-                    _mm(G, Yc, dX[r0:r1])
+                    _mm_nt(G, Yt, dX[r0:r1])
                 if ds is not None:
                     parts.append(ds)
             if want_ds:
@@ -268,7 +278,7 @@ class ScaledLogitsCE(torch.autograd.Function):
                 # transposed problem: rows = columns c0..c1 of S, columns = rows of S
                 GT, _ = ce_fused_grad(Yc[c0:c1], Xc, sc, lse_c[c0:c1] if has_c else None, lse_r, col_off + c0,
                                       coef_c, row_off - c0, coef_r, gout, gdt)
-                _mm(GT, Xc, dY[c0:c1])
+                _mm_nt(GT, Xt, dY[c0:c1])
             dY = dY.to(ydt)
         dS = dscale.to(sdt).reshape(sshape) if want_ds else None
         return dX, dY, dS, None, None, None, None

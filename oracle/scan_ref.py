@@ -61,12 +61,15 @@ def selective_scan_ref(u, delta, A, B, C, D=None, z=None, delta_bias=None,
     Cf = _expand_groups(C.to(cd), dim)
     state = uf.new_zeros(batch, dim, A.shape[1])
     ys = []
+    # per-position views via unbind: its backward is one stack, where indexing [..., t] would
+    # build a full-size zero gradient per step (minutes at L = 4096 under autograd)
+    dts, us, Bts, Cts = dt.unbind(-1), uf.unbind(-1), Bf.unbind(-1), Cf.unbind(-1)
     for t in range(L):
-        d_t = dt[:, :, t].unsqueeze(-1)                       # (B, D, 1)
+        d_t = dts[t].unsqueeze(-1)                            # (B, D, 1)
         decay = torch.exp(d_t * Af)                           # (B, D, N)
-        drive = d_t * Bf[:, :, :, t] * uf[:, :, t].unsqueeze(-1)
+        drive = d_t * Bts[t] * us[t].unsqueeze(-1)
         state = decay * state + drive
-        ys.append((state * Cf[:, :, :, t]).sum(-1))
+        ys.append((state * Cts[t]).sum(-1))
     y = torch.stack(ys, dim=-1) if L > 0 else uf.new_zeros(batch, dim, 0)
     if D is not None:
         y = y + uf * D.to(cd)[:, None]
