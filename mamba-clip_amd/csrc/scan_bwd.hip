@@ -804,6 +804,16 @@ static void launch_reduce_t(const BwdArgs& a, void* dB, void* dC, float* dA, flo
 }  // namespace scan
 }  // namespace mc
 
+namespace mc {
+namespace scan {
+// scan_bwd_pair.hip: the lane-pair kernel for 16-bit rows with dstate 16 (the text towers)
+bool bwd_pair_ok(const mc_scan_bwd_params* p);
+int bwd_pair_nblk(int H);
+void launch_bwd_pair(const mc_scan_bwd_params* p, float* slab_bc, float* slab_a, float* slab_d, float* slab_bias,
+                     int nblk, hipStream_t s);
+}  // namespace scan
+}  // namespace mc
+
 using namespace mc;
 using namespace mc::scan;
 
@@ -851,6 +861,25 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
            p->workspace_bytes);
   char* ws = reinterpret_cast<char*>(p->workspace);
   hipError_t e;
+  if (!dirs && bwd_pair_ok(p)) {
+    // lane-pair kernel: reads 16-bit B / C rows directly (no quad relayout); one slab per 128 channels
+    BwdArgs a{};
+    a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
+    a.nblk = bwd_pair_nblk(p->dim / p->n_groups);
+    a.slab_bc = reinterpret_cast<float*>(ws + w.slab_bc);
+    a.slab_a = reinterpret_cast<float*>(ws + w.slab_a);
+    a.slab_d = reinterpret_cast<float*>(ws + w.slab_d);
+    a.slab_bias = reinterpret_cast<float*>(ws + w.slab_bias);
+    launch_bwd_pair(p, a.slab_bc, a.slab_a, a.slab_d, a.slab_bias, a.nblk, s);
+    e = hipGetLastError();
+    MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: launch failed: %s", hipGetErrorString(e));
+    if (p->wtype == MC_DTYPE_F32) launch_reduce_t<float>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    else if (p->wtype == MC_DTYPE_BF16) launch_reduce_t<bf16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    else launch_reduce_t<f16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    e = hipGetLastError();
+    MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: reduce launch failed: %s", hipGetErrorString(e));
+    return MC_OK;
+  }
   f32x4* bq = reinterpret_cast<f32x4*>(ws + w.bq);
   if (p->wtype == MC_DTYPE_F32) e = launch_bc_quads<float>(p, np, bq, s);
   else if (p->wtype == MC_DTYPE_BF16) e = launch_bc_quads<bf16_t>(p, np, bq, s);

@@ -182,6 +182,41 @@ struct RowLayout {
   static constexpr int kStride = kBytes + 16;
 };
 
+// Packed (two positions) softplus and silu (the lane-pair kernels, scan_fwd_pair.hip / scan_bwd_pair.hip): the arithmetic around the transcendental
+// ops runs as v_pk_* (one issue for two positions).
+__device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
+  // softplus(x) = max(x, 0) + log1p(exp(-|x|)): exp never overflows, and above 20 the log1p
+  // term is below half an ulp of x, which is torch's threshold (x > 20 -> x) exactly.
+  // -|arg| is a free VOP3 input modifier on v_exp_f32.
+  const f32x2 arg = x * kLog2e;
+  const f32x2 t = f32x2{fast_exp2(-fabsf(arg.x)), fast_exp2(-fabsf(arg.y))};
+  const f32x2 tp = t + 1.f;
+  const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)};
+  return lg * kLn2 + f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
+}
+// a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
+// (the compiler otherwise moves an odd-register scalar to an even register first)
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
+  f32x2 r;
+  if constexpr (kHi) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(s));
+  else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(s));
+  return r;
+}
+// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
+  f32x2 r;
+  if constexpr (kHi) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f32x2 silu2(f32x2 z) {
+  const f32x2 arg = z * -kLog2e;
+  const f32x2 ep = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)} + 1.f;
+  return z * f32x2{fast_rcp(ep.x), fast_rcp(ep.y)};
+}
+
 // Forward kernel arguments (scan_fwd.hip, scan_fwd_pair.hip).
 struct FwdArgs {
   int batch, dim, seqlen, dstate, n_groups, n_chunks, n_states, nblk, total_blocks;

@@ -65,7 +65,8 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
 
     ``want_y`` (with z): also return the pre-gate output y + D u -- upstream's
     forward returns it as ``out`` next to ``out_z``.  Training does not need it:
-    the backward recomputes y from the chunk states.
+    the backward recomputes y from the chunk states (saving it measured slower:
+    +1.6 GB of forward writes at C4 for less backward work).
     """
     lib = _lib.load()
     batch, dim, L = delta.shape
