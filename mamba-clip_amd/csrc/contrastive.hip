@@ -27,6 +27,12 @@
 #include "mc_common.h"
 #include "../../include/mc_contrastive.h"
 
+#ifndef MC_SIM_EXP
+#define MC_SIM_EXP 0
+#endif
+#ifndef MC_NT_STORE
+#define MC_NT_STORE 0
+#endif
 namespace mc {
 namespace ctr {
 
@@ -463,7 +469,11 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
         const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c4;
         TOut* dst = C + (int64_t)row * g.ldc + col;
         if (full) {
+#if MC_NT_STORE
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));   // streamed: nothing re-reads it here
+#else
+          *reinterpret_cast<f32x4*>(dst) = v;
+#endif
         } else if (row < g.M) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -484,7 +494,11 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
                               bits16<TOut>(v0[2]) | (bits16<TOut>(v0[3]) << 16),
                               bits16<TOut>(v1[0]) | (bits16<TOut>(v1[1]) << 16),
                               bits16<TOut>(v1[2]) | (bits16<TOut>(v1[3]) << 16)};
+#if MC_NT_STORE
           __builtin_nontemporal_store(pk, reinterpret_cast<u32x4_t*>(dst));
+#else
+          *reinterpret_cast<u32x4_t*>(dst) = pk;
+#endif
         } else if (row < g.M) {
 #pragma unroll
           for (int e = 0; e < 8; ++e)
@@ -493,6 +507,192 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const GemmArgs g) {
       }
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ fp8 similarity (config 5)
+// C = alpha * sa[m] * sb[n] * A B^T for fp8 e4m3 rows with K % 128 == 0 (the C5 similarity:
+// N = 8192, K = E = 512).  Same 128 x 128 tile / 4-wave decomposition as gemm_nt_kernel, but:
+//  * K steps of 128 bytes on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit block
+//    scales): twice the non-scaled fp8 MFMA rate, 16 MFMAs per wave and step;
+//  * operands land in LDS by global_load_lds (16 B per lane, no VGPR round trip), two steps in
+//    flight, waited with a counted vmcnt and a raw s_barrier (no vmcnt(0) drain per step);
+//  * the LDS image is lane-linear (glds), so the bank swizzle sits on the SOURCE chunk and the
+//    matching read: chunk c of row r lives at slot c ^ ((r >> 1) & 7) -- sixteen consecutive rows
+//    reading one chunk hit sixteen distinct 4-bank groups;
+//  * plain (not non-temporal) 16-B epilogue stores: the 268 MB fp32 logit matrix streams at
+//    6.9 TB/s with plain stores vs 5.2-5.9 non-temporal (tools/ubench/hbm_rw.hip).
+constexpr int kSBK = 128;                      // K bytes per step
+constexpr int kSStage = 2 * BM * kSBK;         // A + B bytes per stage (32 KB)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// One global_load_lds_dwordx4: 16 B per lane from gsrc to LDS byte address m0v + 16 * lane
+// (m0v wave-uniform).  Written as asm so hipcc does not track it: its waitcnt pass would otherwise
+// drain every in-flight LDS-DMA with vmcnt(0) before the first ds_read of each K step.  The caller
+// counts completion with its own vmcnt.  M0 is compiler-reserved: saved and restored in the statement.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0v) : "memory");
+}
+
+template <typename TOut>
+__global__ __launch_bounds__(256, 2) void sim_fp8_kernel(const GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kSStage];   // the only LDS object (glds + epilogue)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  constexpr int kGroupM = 8;
+  const int bid = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
+  const int first_m = (bid / (kGroupM * g.tiles_n)) * kGroupM;
+  const int gm = min(g.tiles_m - first_m, kGroupM);
+  const int local = bid % (kGroupM * g.tiles_n);
+  const int tm = first_m + local % gm, tn = local / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const uint8_t* __restrict__ A = reinterpret_cast<const uint8_t*>(g.A);
+  const uint8_t* __restrict__ B = reinterpret_cast<const uint8_t*>(g.B);
+
+  // glds: wave w, instruction j, lane l -> chunk q = (4w + j) * 64 + l of a 128-row slice image:
+  // row q >> 3, slot q & 7, loading the row's chunk (slot ^ swz(row)) (rows past M / N clamped)
+  const uint8_t* srcA[4];
+  const uint8_t* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = (4 * w + j) * 64 + lane, r = q >> 3, slot = q & 7;
+    const int c = slot ^ ((r >> 1) & 7);
+    srcA[j] = A + (int64_t)min(m0 + r, g.M - 1) * g.lda + c * 16;
+    srcB[j] = B + (int64_t)min(n0 + r, g.N - 1) * g.ldb + c * 16;
+  }
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds_w = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)(lds) + 4 * 1024 * w);
+  auto issue = [&](int step) __attribute__((always_inline)) {   // one K step into buffer step & 1
+    const uint32_t la = lds_w + (step & 1) * kSStage, lb = la + BM * kSBK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      glds16_asm(srcA[j] + step * kSBK, la + j * 1024);
+      glds16_asm(srcB[j] + step * kSBK, lb + j * 1024);
+    }
+  };
+
+  const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
+  float col_scale[4], row_scale[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wc * 64 + j * 16 + (lane & 15);
+    col_scale[j] = (g.sb && col < g.N) ? g.sb[col] : 1.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+      row_scale[i][r] = (g.sa && row < g.M) ? g.sa[row] : 1.f;
+    }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#if MC_SIM_EXP == 2
+  const int nk = 0;
+#else
+  const int nk = g.K / kSBK;
+#endif
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  // fragment read offsets: lane row (l & 15) of a 16-row tile, K bytes [32 (l >> 4), +32) = chunks 2g, 2g + 1
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int s = 0; s < nk; ++s) {
+    // this wave's glds of step s done (step s + 1's 8 may stay in flight), then everyone's
+    if (s + 1 < nk) __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8)
+    else __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    const char* la = lds + (s & 1) * kSStage;
+    const char* lb = la + BM * kSBK;
+    i32x8 af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra = wr * 64 + i * 16 + fr, rb = wc * 64 + i * 16 + fr;
+      const int sa = (ra >> 1) & 7, sb = (rb >> 1) & 7;
+      const uint4 a0 = *reinterpret_cast<const uint4*>(la + ra * kSBK + (((2 * fg) ^ sa) << 4));
+      const uint4 a1 = *reinterpret_cast<const uint4*>(la + ra * kSBK + (((2 * fg + 1) ^ sa) << 4));
+      const uint4 b0 = *reinterpret_cast<const uint4*>(lb + rb * kSBK + (((2 * fg) ^ sb) << 4));
+      const uint4 b1 = *reinterpret_cast<const uint4*>(lb + rb * kSBK + (((2 * fg + 1) ^ sb) << 4));
+      af[i] = i32x8{(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+      bf[i] = i32x8{(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bf[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();         // ... and everyone's: the buffer can be refilled
+    if (s + 2 < nk) issue(s + 2);
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = (acc[i][j][r] * row_scale[i][r]) * (alpha * col_scale[j]);
+
+  // epilogue through LDS (as gemm_nt_kernel): 32 x 64 per wave and pass, 16-B stores
+  TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
+  constexpr int kEpStride = 68;
+  float* ep = reinterpret_cast<float*>(lds) + w * (32 * kEpStride);
+  const bool full = g.c_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i2 * 16 + 4 * (lane >> 4) + r) * kEpStride + j * 16 + (lane & 15)] = acc[2 * p + i2][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (sizeof(TOut) == 4) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int q = lane + 64 * t;
+        const int row_l = q >> 4, c4 = (q & 15) * 4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c4);
+        const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c4;
+        TOut* dst = C + (int64_t)row * g.ldc + col;
+#if MC_SIM_EXP == 1
+        if (v[0] == 1234.5f) *reinterpret_cast<f32x4*>(dst) = v;
+#else
+        if (full) {
+          *reinterpret_cast<f32x4*>(dst) = v;
+        } else if (row < g.M) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < g.N) dst[e] = v[e];
+        }
+#endif
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int q = lane + 64 * t;
+        const int row_l = q >> 3, c8 = (q & 7) * 8;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row_l * kEpStride + c8 + 4);
+        const int row = m0 + wr * 64 + p * 32 + row_l, col = n0 + wc * 64 + c8;
+        TOut* dst = C + (int64_t)row * g.ldc + col;
+        if (full && g.c_vec16) {
+          *reinterpret_cast<uint4*>(dst) = make_uint4(cvt_pk2<TOut>(v0[0], v0[1]), cvt_pk2<TOut>(v0[2], v0[3]),
+                                                      cvt_pk2<TOut>(v1[0], v1[1]), cvt_pk2<TOut>(v1[2], v1[3]));
+        } else if (row < g.M) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (col + e < g.N) dst[e] = from_f<TOut>(e < 4 ? v0[e] : v1[e - 4]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's staging reads done before the next pass writes
   }
 }
 
@@ -770,7 +970,13 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   g.sa = p->row_scale_a; g.sb = p->row_scale_b;
   g.c_vec = aligned16(p->C) && p->ldc % 4 == 0;
   g.c_vec16 = g.c_vec && p->ldc % 8 == 0;
-  launch_gemm<0>(g, p->in_dtype, p->out_dtype, aligned, (hipStream_t)stream);
+  if (p->in_dtype == MC_DTYPE_FP8_E4M3 && p->K % kSBK == 0 && p->K > 0) {   // the C5 similarity path
+    const dim3 grid(g.tiles_m * g.tiles_n), block(256);
+    if (p->out_dtype == MC_DTYPE_F32) hipLaunchKernelGGL(sim_fp8_kernel<float>, grid, block, 0, (hipStream_t)stream, g);
+    else hipLaunchKernelGGL(sim_fp8_kernel<bf16_t>, grid, block, 0, (hipStream_t)stream, g);
+  } else {
+    launch_gemm<0>(g, p->in_dtype, p->out_dtype, aligned, (hipStream_t)stream);
+  }
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_nt: launch failed: %s", hipGetErrorString(e));
   return MC_OK;

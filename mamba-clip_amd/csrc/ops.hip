@@ -1012,7 +1012,8 @@ extern "C" int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, i
 
 // ------------------------------------------------------------------ achievable HBM rate (measurement)
 // float4 streaming copy: each thread moves kU 16-B vectors per pass (loads first, then stores, so
-// kU loads are in flight per lane); grid sized to ~8 waves per CU's worth of work per pass.
+// kU loads are in flight per lane); up to 65536 blocks (tools/ubench/hbm_rw.hip: the larger grid
+// streams fastest, 5.85 TB/s at 2 GiB vs 5.1 at 1024 blocks).
 namespace {
 constexpr int kCopyU = 4;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -1040,7 +1041,7 @@ extern "C" int mc_stream_copy(const void* src, void* dst, size_t nbytes, void* s
            "mc_stream_copy: 16-B aligned buffers and a multiple of 16 bytes required");
   if (nbytes == 0) return MC_OK;
   const int64_t n16 = (int64_t)(nbytes / 16);
-  const int grid = (int)std::min<int64_t>((n16 + 256 * kCopyU - 1) / (256 * kCopyU), 256 * 32);
+  const int grid = (int)std::min<int64_t>((n16 + 256 * kCopyU - 1) / (256 * kCopyU), 65536);
   hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const u32x4_t*>(src), reinterpret_cast<u32x4_t*>(dst), n16);
   return check_launch("mc_stream_copy");
