@@ -104,6 +104,24 @@ typedef struct mc_scan_fwd_params {
    *                 blocks [x, x^T]); 0 = u has dim rows as usual.
    * Either set: z must be NULL (the cross-scan has no gate). */
   int32_t reverse_groups, u_groups;
+  /* Projected delta -- the Mamba mixer's dt_proj fused into the scan (reference
+   * model.py:519-528 / 630-647; upstream's mamba_inner_fn analogue).  When
+   * delta_proj_w is non-NULL, `delta` is not read; instead
+   *     delta[b, d, l] = sum_r delta_proj_w[d * dpw_dim_stride + r]
+   *                          * delta_proj_x[b * dpx_batch_stride + l * dpx_token_stride + r]
+   * is formed per chunk on the matrix cores, rounded to itype (what a dt_proj
+   * GEMM would store), so the (batch, dim, seqlen) delta stream never leaves
+   * the chip.  Both operands are itype; delta_proj_x is token-major.
+   * delta_rank % 16 == 0, 16..256; 8-B aligned operands, strides % 4 == 0.
+   * Pair-kernel shapes only (16-bit rows, dstate 16, seqlen % 8 == 0, 16-B
+   * aligned rows, no grouped directions), else MC_ERR_SHAPE.
+   * delta_out (nullable): the formed delta, written with delta_batch_stride /
+   * delta_dim_stride -- the input mc_scan_bwd needs for training. */
+  const void* delta_proj_x;
+  const void* delta_proj_w;
+  int32_t delta_rank;
+  int64_t dpx_batch_stride, dpx_token_stride, dpw_dim_stride;
+  void* delta_out;
 } mc_scan_fwd_params;
 
 typedef struct mc_scan_bwd_params {
@@ -154,6 +172,13 @@ typedef struct mc_scan_bwd_params {
    * u_groups > 0, du still has dim rows (one per group and channel): the caller
    * sums the groups that share a u block. */
   int32_t reverse_groups, u_groups;
+  /* Projected delta (see mc_scan_fwd_params): when delta_proj_w is non-NULL,
+   * `delta` is not read; the kernel re-forms it per chunk from the same
+   * operands, bit-identical to the forward's.  Same requirements. */
+  const void* delta_proj_x;
+  const void* delta_proj_w;
+  int32_t delta_rank;
+  int64_t dpx_batch_stride, dpx_token_stride, dpw_dim_stride;
 } mc_scan_bwd_params;
 
 /* number of MC_SCAN_CHUNK-long chunks covering seqlen */

@@ -839,8 +839,20 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
     if (p->ddelta_bias) (void)hipMemsetAsync(p->ddelta_bias, 0, (size_t)p->dim * 4, s);
     return MC_OK;
   }
-  MC_CHECK(p->u && p->delta && p->B && p->C && p->dout && p->du && p->ddelta && p->dB && p->dC, MC_ERR_INVALID,
-           "mc_scan_bwd: u, delta, B, C, dout and du, ddelta, dB, dC must be non-null");
+  const bool proj = p->delta_proj_w != nullptr;
+  MC_CHECK(p->u && (p->delta || proj) && p->B && p->C && p->dout && p->du && p->ddelta && p->dB && p->dC,
+           MC_ERR_INVALID, "mc_scan_bwd: u, delta (or delta_proj_*), B, C, dout and du, ddelta, dB, dC must be non-null");
+  if (proj) {
+    const int64_t R = p->delta_rank;
+    MC_CHECK(p->delta_proj_x && R >= 16 && R <= 256 && R % 16 == 0 && p->dpx_token_stride >= R &&
+                 p->dpx_token_stride % 4 == 0 && p->dpx_batch_stride % 4 == 0 && p->dpw_dim_stride >= R &&
+                 p->dpw_dim_stride % 4 == 0 && reinterpret_cast<uintptr_t>(p->delta_proj_x) % 8 == 0 &&
+                 reinterpret_cast<uintptr_t>(p->delta_proj_w) % 8 == 0 &&
+                 ((int64_t)(p->seqlen - 1) * p->dpx_token_stride + R) * 2 < ((int64_t)1 << 31) &&
+                 (31 * p->dpw_dim_stride + R) * 2 < ((int64_t)1 << 31),
+             MC_ERR_SHAPE, "mc_scan_bwd: projected delta needs delta_proj_x, delta_rank in [16, 256] (a multiple "
+             "of 16), 8-B aligned operands with strides %% 4 == 0 and 32-bit spans (got rank %d)", p->delta_rank);
+  }
   MC_CHECK(!p->z || p->dz, MC_ERR_INVALID, "mc_scan_bwd: dz required when z is given");
   MC_CHECK((int64_t)kRows * mc_scan_n_chunks(p->seqlen) * p->dstate * 4 < ((int64_t)1 << 31) &&
                (int64_t)p->seqlen * (np / 2) * 16 < ((int64_t)1 << 31) &&
@@ -861,6 +873,9 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
            p->workspace_bytes);
   char* ws = reinterpret_cast<char*>(p->workspace);
   hipError_t e;
+  MC_CHECK(!proj || (!dirs && bwd_pair_ok(p)), MC_ERR_SHAPE,
+           "mc_scan_bwd: projected delta needs the pair kernel's shapes (16-bit rows, dstate 16, seqlen %% 8 == 0, "
+           "16-B aligned rows, no grouped directions)");
   if (!dirs && bwd_pair_ok(p)) {
     // lane-pair kernel: reads 16-bit B / C rows directly (no quad relayout); one slab per 128 channels
     BwdArgs a{};

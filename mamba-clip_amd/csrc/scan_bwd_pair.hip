@@ -54,6 +54,9 @@ struct BwdPairArgs {
   float* slab_a;      // [b][16][dim]
   float* slab_d;      // [b][dim]
   float* slab_bias;   // [b][dim]
+  // projected delta (mc_scan.h): delta re-formed per chunk from dpx / dpw, as the forward did
+  const void* dpx; const void* dpw; int rank;
+  int64_t dpx_bs, dpx_ts, dpw_ds;
 };
 
 // quad_perm DPP move (bound_ctrl: a disabled source reads 0 -- never the case here)
@@ -117,7 +120,7 @@ __device__ __forceinline__ f32x2 elem2(uint2 w, int i) {   // elements 2i, 2i + 
   return f32x2{elem_f<TI>(q, 2 * i), elem_f<TI>(q, 2 * i + 1)};
 }
 
-template <typename TI, bool kSP, bool kZ>
+template <typename TI, bool kSP, bool kZ, bool kPD>
 __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPairArgs a) {
   using TW = TI;                               // B / C in the activation dtype (x_dbl rows)
   constexpr int kWV = 16 / (int)sizeof(TW);   // B / C elements per 16-B vector
@@ -130,6 +133,9 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   f32x4* bcq = reinterpret_cast<f32x4*>(smem) + wave * (kS * 2 * kQP);                    // [t][h][p]
   float* dbc_base = reinterpret_cast<float*>(smem + (size_t)kQW * kS * 2 * kQP * 16);     // [buf][wave][t][2][16]
   f32x4* xst = reinterpret_cast<f32x4*>(dbc_base + 2 * kQW * kDbcW) + wave * ((kQSub - 1) * 2 * 64);   // [s][2][lane]
+  // projected delta: this wave's chunk tile [channel][position] in the activation dtype (2 KB)
+  char* dlt = reinterpret_cast<char*>(reinterpret_cast<f32x4*>(dbc_base + 2 * kQW * kDbcW) + kQW * ((kQSub - 1) * 2 * 64)) +
+              wave * (kQCh * kS * 2);
 
   const int lin = xcd_remap(blockIdx.x, a.total_blocks);
   const int wblk = lin % a.nblk;
@@ -176,6 +182,14 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(a.chunk_states + ((int64_t)b * a.dim + dbase) * cs_row,
                                                  (uint32_t)nrows * cs_row * 4u);
 
+  // projected delta operands: token-major dpx rows of this batch, the wave's dpw rows
+  const __amdgpu_buffer_rsrc_t rs_px =
+      make_rsrc(kPD ? reinterpret_cast<const TI*>(a.dpx) + (int64_t)b * a.dpx_bs : reinterpret_cast<const TI*>(a.u),
+                kPD ? (uint32_t)(((int64_t)(L_ - 1) * a.dpx_ts + a.rank) * (int64_t)sizeof(TI)) : 0u);
+  const __amdgpu_buffer_rsrc_t rs_pw =
+      make_rsrc(kPD ? reinterpret_cast<const TI*>(a.dpw) + (int64_t)dbase * a.dpw_ds : reinterpret_cast<const TI*>(a.u),
+                kPD && nrows > 0 ? (uint32_t)(((int64_t)(nrows - 1) * a.dpw_ds + a.rank) * (int64_t)sizeof(TI)) : 0u);
+
   // ---- lane constants: pairs (8h + 2p, 8h + 2p + 1) of channel my_dc
   f32x2 A2[kQP], hcar[kQP], dA2[kQP];
 #pragma unroll
@@ -208,7 +222,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   auto load_raw = [&](int pos) __attribute__((always_inline)) {   // pos: first position of the sub-tile
     const uint32_t e = (uint32_t)(pos + 4 * h);
     nu = buf_ld8<TI>(rs_u, (ro_u + e) * 2u);
-    nd = buf_ld8<TI>(rs_d, (ro_d + e) * 2u);
+    if constexpr (!kPD) nd = buf_ld8<TI>(rs_d, (ro_d + e) * 2u);
     ng = buf_ld8<TI>(rs_g, (ro_g + e) * 2u);
     if constexpr (hasZ) {
       nz = buf_ld8<TI>(rs_z, (ro_z + e) * 2u);
@@ -277,6 +291,40 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
           dst[t * (2 * kQP * 4) + 2] = elem_f<TW>(pC[k], e);
         }
     }
+    if constexpr (kPD) {   // the chunk's delta tile, formed exactly as scan_fwd_pair_kernel does
+      using MM = Mfma16<TI>;
+      const int i16 = lane & 15, q4 = 4 * (lane >> 4);
+      const int nr = max(nrows, 1);
+      f32x4 dacc[2][2];
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) dacc[pb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t xo0 = (uint32_t)((l0 + i16) * a.dpx_ts + q4) * (uint32_t)sizeof(TI);
+      const uint32_t xo1 = (uint32_t)((l0 + 16 + i16) * a.dpx_ts + q4) * (uint32_t)sizeof(TI);
+      const uint32_t wo0 = (uint32_t)(min(i16, nr - 1) * a.dpw_ds + q4) * (uint32_t)sizeof(TI);
+      const uint32_t wo1 = (uint32_t)(min(16 + i16, nr - 1) * a.dpw_ds + q4) * (uint32_t)sizeof(TI);
+#pragma unroll 2
+      for (int r0 = 0; r0 < a.rank; r0 += 16) {
+        const uint32_t ro = (uint32_t)r0 * (uint32_t)sizeof(TI);
+        const auto x0v = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_px, xo0 + ro, 0, 0));
+        const auto x1v = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_px, xo1 + ro, 0, 0));
+        const auto w0 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_pw, wo0 + ro, 0, 0));
+        const auto w1 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_pw, wo1 + ro, 0, 0));
+        dacc[0][0] = MM::mma(x0v, w0, dacc[0][0]);
+        dacc[0][1] = MM::mma(x0v, w1, dacc[0][1]);
+        dacc[1][0] = MM::mma(x1v, w0, dacc[1][0]);
+        dacc[1][1] = MM::mma(x1v, w1, dacc[1][1]);
+      }
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const uint2 v = make_uint2(bits16<TI>(dacc[pb][cb][0]) | (bits16<TI>(dacc[pb][cb][1]) << 16),
+                                     bits16<TI>(dacc[pb][cb][2]) | (bits16<TI>(dacc[pb][cb][3]) << 16));
+          *reinterpret_cast<uint2*>(dlt + ((16 * cb + i16) * kS + 16 * pb + q4) * 2) = v;
+        }
+    }
     f32x2 x0[kQP];
     x0[0] = px[0].lo; x0[1] = px[0].hi; x0[2] = px[1].lo; x0[3] = px[1].hi;
     if (!my_ok) {
@@ -293,7 +341,8 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
       for (int p = 0; p < kQP; ++p) x[p] = x0[p];
 #pragma unroll 1
       for (int s = 0; s + 1 < nsub; ++s) {
-        const uint2 ru = nu, rd = nd, rz = nz, rg = ng;
+        const uint2 ru = nu, rz = nz, rg = ng;
+        const uint2 rd = kPD ? *reinterpret_cast<const uint2*>(dlt + (my_r * kS + kQT * s + 4 * h) * 2) : nd;
         load_raw(l0 + kQT * (s + 1));
         Sc sc;
         scalars(ru, rd, rz, rg, false, sc);
@@ -318,7 +367,8 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
     // ---- sub-tiles in reverse
 #pragma unroll 1
     for (int s = nsub - 1; s >= 0; --s) {
-      const uint2 ru = nu, rd = nd, rz = nz, rg = ng;
+      const uint2 ru = nu, rz = nz, rg = ng;
+      const uint2 rd = kPD ? *reinterpret_cast<const uint2*>(dlt + (my_r * kS + kQT * s + 4 * h) * 2) : nd;
       load_raw(s > 0 ? l0 + kQT * (s - 1) : l0 - kS);   // next step (next chunk's first sub-tile after s = 0)
       Sc sc;
       scalars(ru, rd, rz, rg, true, sc);
@@ -489,8 +539,11 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   }
 }
 
-size_t bwd_pair_lds_bytes() {   // B / C quads, dB / dC partials (double-buffered), sub-tile states: 72 KB
-  return (size_t)kQW * kS * 2 * kQP * 16 + (size_t)2 * kQW * kS * 2 * kQN * 4 + (size_t)kQW * (kQSub - 1) * 2 * 64 * 16;
+// B / C quads, dB / dC partials (double-buffered), sub-tile states: 72 KB; + the projected-delta tiles
+// (2 KB per wave): 80 KB, still two workgroups per CU
+size_t bwd_pair_lds_bytes(bool proj) {
+  return (size_t)kQW * kS * 2 * kQP * 16 + (size_t)2 * kQW * kS * 2 * kQN * 4 + (size_t)kQW * (kQSub - 1) * 2 * 64 * 16 +
+         (proj ? (size_t)kQW * kQCh * kS * 2 : 0);
 }
 int bwd_pair_nblk(int H) { return (H + kQCh * kQW - 1) / (kQCh * kQW); }
 
@@ -509,7 +562,8 @@ bool bwd_pair_ok(const mc_scan_bwd_params* p) {
     return aligned16(t) && bs % v == 0 && gs % v == 0 && ns % v == 0 && ns >= 0 &&
            (15 * ns + p->seqlen) * wb < ((int64_t)1 << 31);
   };
-  return rows(p->u, p->u_batch_stride, p->u_dim_stride) && rows(p->delta, p->delta_batch_stride, p->delta_dim_stride) &&
+  return rows(p->u, p->u_batch_stride, p->u_dim_stride) &&
+         (p->delta_proj_w || rows(p->delta, p->delta_batch_stride, p->delta_dim_stride)) &&
          rows(p->z, p->z_batch_stride, p->z_dim_stride) && rows(p->dout, p->dout_batch_stride, p->dout_dim_stride) &&
          rows(p->du, p->du_batch_stride, p->du_dim_stride) &&
          rows(p->ddelta, p->ddelta_batch_stride, p->ddelta_dim_stride) &&
@@ -519,14 +573,19 @@ bool bwd_pair_ok(const mc_scan_bwd_params* p) {
          (int64_t)kQCh * kQW * mc_scan_n_chunks(p->seqlen) * kQN * 4 < ((int64_t)1 << 31);
 }
 
+template <typename TI, bool kPD>
+static void launch_pair_pd(const BwdPairArgs& a, bool sp, bool zy, hipStream_t s) {
+  const size_t lds = bwd_pair_lds_bytes(kPD);
+  const dim3 grid(a.total_blocks), block(64 * kQW);
+  if (sp && zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, true, kPD>), grid, block, lds, s, a);
+  else if (sp) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, false, kPD>), grid, block, lds, s, a);
+  else if (zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, true, kPD>), grid, block, lds, s, a);
+  else hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, false, kPD>), grid, block, lds, s, a);
+}
 template <typename TI>
 static void launch_pair_t(const BwdPairArgs& a, bool sp, bool zy, hipStream_t s) {
-  const size_t lds = bwd_pair_lds_bytes();
-  const dim3 grid(a.total_blocks), block(64 * kQW);
-  if (sp && zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, true>), grid, block, lds, s, a);
-  else if (sp) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, false>), grid, block, lds, s, a);
-  else if (zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, true>), grid, block, lds, s, a);
-  else hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, false>), grid, block, lds, s, a);
+  if (a.dpw) launch_pair_pd<TI, true>(a, sp, zy, s);
+  else launch_pair_pd<TI, false>(a, sp, zy, s);
 }
 
 void launch_bwd_pair(const mc_scan_bwd_params* p, float* slab_bc, float* slab_a, float* slab_d, float* slab_bias,
@@ -549,6 +608,8 @@ void launch_bwd_pair(const mc_scan_bwd_params* p, float* slab_bc, float* slab_a,
   a.A = p->A; a.D = p->D; a.delta_bias = p->delta_bias; a.chunk_states = p->chunk_states;
   a.du = p->du; a.ddelta = p->ddelta; a.dz = p->dz;
   a.slab_bc = slab_bc; a.slab_a = slab_a; a.slab_d = slab_d; a.slab_bias = slab_bias;
+  a.dpx = p->delta_proj_x; a.dpw = p->delta_proj_w; a.rank = p->delta_rank;
+  a.dpx_bs = p->dpx_batch_stride; a.dpx_ts = p->dpx_token_stride; a.dpw_ds = p->dpw_dim_stride;
   const bool sp = p->delta_softplus != 0, zy = p->z != nullptr;
   if (p->itype == MC_DTYPE_BF16) launch_pair_t<bf16_t>(a, sp, zy, s);
   else launch_pair_t<f16_t>(a, sp, zy, s);

@@ -218,6 +218,17 @@ __device__ __forceinline__ f32x2 silu2(f32x2 z) {
 }
 
 // Forward kernel arguments (scan_fwd.hip, scan_fwd_pair.hip).
+// MFMA operand vectors of the projected-delta tile (4 16-bit values per lane)
+template <typename TI> struct Mfma16;
+template <> struct Mfma16<bf16_t> {
+  typedef short v4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ f32x4 mma(v4 a, v4 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
+};
+template <> struct Mfma16<f16_t> {
+  typedef _Float16 v4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ f32x4 mma(v4 a, v4 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+};
+
 struct FwdArgs {
   int batch, dim, seqlen, dstate, n_groups, n_chunks, n_states, nblk, total_blocks;
   int softplus;
@@ -227,6 +238,10 @@ struct FwdArgs {
   void* out; float* chunk_states; float* last_state;
   void* out_y; int64_t y_bs, y_ds;   // nullable: pre-gate y + D u (training with z: the backward's dz input)
   int rev_groups, u_groups;          // grouped directions (0 = off; element-wise path only)
+  // projected delta (pair kernel only): delta = dpw (dim x rank) . dpx^T, formed per chunk on MFMA
+  const void* dpx; const void* dpw; int rank;
+  int64_t dpx_bs, dpx_ts, dpw_ds;
+  void* delta_out;                   // nullable: the formed delta, strides dt_bs / dt_ds
 };
 
 int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who);

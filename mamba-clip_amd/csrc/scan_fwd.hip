@@ -754,8 +754,23 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
       (void)hipMemsetAsync(p->last_state, 0, (size_t)p->batch * p->dim * p->dstate * 4, s);
     return MC_OK;
   }
-  MC_CHECK(p->u && p->delta && p->A && p->B && p->C && p->out, MC_ERR_INVALID,
-           "mc_scan_fwd: u, delta, A, B, C and out must be non-null");
+  const bool proj = p->delta_proj_w != nullptr;
+  MC_CHECK(p->u && (p->delta || proj) && p->A && p->B && p->C && p->out, MC_ERR_INVALID,
+           "mc_scan_fwd: u, delta (or delta_proj_w / delta_proj_x), A, B, C and out must be non-null");
+  if (proj) {
+    const int64_t L = p->seqlen, R = p->delta_rank;
+    MC_CHECK(p->delta_proj_x && R >= 16 && R <= 256 && R % 16 == 0, MC_ERR_SHAPE,
+             "mc_scan_fwd: projected delta needs delta_proj_x and delta_rank in [16, 256], a multiple of 16 (got %d)",
+             p->delta_rank);
+    MC_CHECK(p->dpx_token_stride >= R && p->dpx_token_stride % 4 == 0 && p->dpx_batch_stride % 4 == 0 &&
+                 p->dpw_dim_stride >= R && p->dpw_dim_stride % 4 == 0 &&
+                 reinterpret_cast<uintptr_t>(p->delta_proj_x) % 8 == 0 &&
+                 reinterpret_cast<uintptr_t>(p->delta_proj_w) % 8 == 0 &&
+                 ((L - 1) * p->dpx_token_stride + R) * 2 < ((int64_t)1 << 31) &&
+                 (31 * p->dpw_dim_stride + R) * 2 < ((int64_t)1 << 31),
+             MC_ERR_SHAPE, "mc_scan_fwd: projected delta operands need 8-B aligned rows (strides %% 4 == 0), "
+             "token stride >= delta_rank and 32-bit spans");
+  }
   const size_t need = bct_bytes(p->batch, p->seqlen, p->dstate, p->n_groups);
   MC_CHECK(p->workspace && p->workspace_bytes >= need && aligned16(p->workspace), MC_ERR_WORKSPACE,
            "mc_scan_fwd: workspace must be >= %zu bytes and 16-B aligned (got %zu)", need, p->workspace_bytes);
@@ -791,14 +806,18 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   a.out = p->out; a.chunk_states = p->chunk_states; a.last_state = p->last_state;
   a.out_y = p->z ? p->out_y : nullptr; a.y_bs = p->out_y_batch_stride; a.y_ds = p->out_y_dim_stride;
   a.rev_groups = dirs ? p->reverse_groups : 0; a.u_groups = dirs ? p->u_groups : 0;
+  a.dpx = p->delta_proj_x; a.dpw = p->delta_proj_w; a.rank = p->delta_rank;
+  a.dpx_bs = p->dpx_batch_stride; a.dpx_ts = p->dpx_token_stride; a.dpw_ds = p->dpw_dim_stride;
+  a.delta_out = proj ? p->delta_out : nullptr;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
-                       vec_ok(p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
+                       vec_ok(proj ? p->delta_out : p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
                        vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
                        vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
   if (dirs) {   // per-group addressing lives in the LDS-staged kernel (vector modes: seqlen % VI == 0)
+    MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta and grouped directions do not combine");
     const bool al = aligned && p->seqlen % (16 / ib) == 0;
     if (p->itype == MC_DTYPE_F32) return launch_fwd_dirs<float>(a, al, s);
     if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
@@ -807,6 +826,8 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
   // forward 0.166 vs 0.183 ms per layer)
   if (fwd_pair_ok(a, aligned, ib)) return launch_fwd_pair(a, p->itype, s);
+  MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta needs the pair kernel's shapes (16-bit rows, "
+           "dstate 16, seqlen %% 8 == 0, 16-B aligned rows, no grouped directions)");
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
   if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
   return launch_fwd_t<f16_t>(a, aligned, s);

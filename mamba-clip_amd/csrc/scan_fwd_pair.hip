@@ -43,7 +43,7 @@ struct PairLayout {
   static constexpr int kBCBytes = kT * 2 * kPN * 4;
 };
 
-template <typename TI, bool kSP, int kMinW>
+template <typename TI, bool kSP, int kMinW, bool kPD>
 __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
   using PL = PairLayout<TI>;
   constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
@@ -72,12 +72,22 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
                      (uint32_t)(((int64_t)(nrows - 1) * ds + L_) * (int64_t)sizeof(TI)));
   };
   const __amdgpu_buffer_rsrc_t rs_u = rows_rsrc(a.u, a.u_bs, a.u_ds);
-  const __amdgpu_buffer_rsrc_t rs_d = rows_rsrc(a.delta, a.dt_bs, a.dt_ds);
+  const __amdgpu_buffer_rsrc_t rs_d = rows_rsrc(kPD ? (a.delta_out ? a.delta_out : a.u) : a.delta,
+                                                kPD && !a.delta_out ? a.u_bs : a.dt_bs, kPD && !a.delta_out ? a.u_ds : a.dt_ds);
   const __amdgpu_buffer_rsrc_t rs_z = rows_rsrc(hasZ ? a.z : a.u, hasZ ? a.z_bs : a.u_bs, hasZ ? a.z_ds : a.u_ds);
   const __amdgpu_buffer_rsrc_t rs_o = rows_rsrc(a.out, a.o_bs, a.o_ds);
   const __amdgpu_buffer_rsrc_t rs_y =
       rows_rsrc(a.out_y ? a.out_y : a.u, a.out_y ? a.y_bs : a.u_bs, a.out_y ? a.y_ds : a.u_ds);
   const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(a.bct + (int64_t)bg * L_ * (2 * kPN), (uint32_t)L_ * (2 * kPN) * 4u);
+
+  // ---- projected delta: token-major dpx rows of this batch (rank values per token, 8-B pieces), the
+  // wave's 32 rows of dpw; tokens past L read 0 (their delta is masked in the staging anyway)
+  const __amdgpu_buffer_rsrc_t rs_px =
+      make_rsrc(kPD ? reinterpret_cast<const TI*>(a.dpx) + (int64_t)b * a.dpx_bs : reinterpret_cast<const TI*>(a.u),
+                kPD ? (uint32_t)(((int64_t)(L_ - 1) * a.dpx_ts + a.rank) * (int64_t)sizeof(TI)) : 0u);
+  const __amdgpu_buffer_rsrc_t rs_pw =
+      make_rsrc(kPD ? reinterpret_cast<const TI*>(a.dpw) + (int64_t)dbase * a.dpw_ds : reinterpret_cast<const TI*>(a.u),
+                kPD ? (uint32_t)(((int64_t)(nrows - 1) * a.dpw_ds + a.rank) * (int64_t)sizeof(TI)) : 0u);
 
   // ---- recurrence lane constants: channel ch, states [8h, 8h + 8)
   const bool my_ok = ch < nrows;
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
 #pragma unroll
     for (int k = 0; k < kNV; ++k) {
       pu[k] = buf_ld16(rs_u, voff(k, a.u_ds, l0));
-      pd[k] = buf_ld16(rs_d, voff(k, a.dt_ds, l0));
+      if constexpr (!kPD) pd[k] = buf_ld16(rs_d, voff(k, a.dt_ds, l0));
     }
 #pragma unroll
     for (int k = 0; k < kBCPer; ++k)
@@ -126,6 +136,48 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
     // chunk that runs past the end (L % kT != 0; L % VI == 0, so whole vectors) the vectors
     // at positions >= L stage dt = du = 0: the state stays frozen, the saved state is the one
     // after L - 1.  A uniform branch picks the masked copy, full chunks carry no selects.
+    if constexpr (kPD) {
+      // delta tile (32 positions x 32 channels) = dpx[l0 .., :] . dpw[rows, :]^T on 16x16x16 MFMAs:
+      // lane (i = lane & 15, q = lane >> 4) feeds position / channel i and ranks [16 ks + 4q, +4), and
+      // gets delta at positions 16 pb + 4q + [0, 4) of channel 16 cb + i.  Rounded to the activation
+      // dtype (what the unfused dt_proj GEMM stores), then parked in the dt slots of the row buffer
+      // for the staging below.
+      using MM = Mfma16<TI>;
+      const int i16 = lane & 15, q4 = 4 * (lane >> 4);
+      f32x4 dacc[2][2];
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) dacc[pb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t xo0 = (uint32_t)((l0 + i16) * a.dpx_ts + q4) * (uint32_t)sizeof(TI);
+      const uint32_t xo1 = (uint32_t)((l0 + 16 + i16) * a.dpx_ts + q4) * (uint32_t)sizeof(TI);
+      const uint32_t wo0 = (uint32_t)(min(i16, nrows - 1) * a.dpw_ds + q4) * (uint32_t)sizeof(TI);
+      const uint32_t wo1 = (uint32_t)(min(16 + i16, nrows - 1) * a.dpw_ds + q4) * (uint32_t)sizeof(TI);
+#pragma unroll 2
+      for (int r0 = 0; r0 < a.rank; r0 += 16) {
+        const uint32_t ro = (uint32_t)r0 * (uint32_t)sizeof(TI);
+        const auto x0 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_px, xo0 + ro, 0, 0));
+        const auto x1 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_px, xo1 + ro, 0, 0));
+        const auto w0 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_pw, wo0 + ro, 0, 0));
+        const auto w1 = __builtin_bit_cast(typename MM::v4, __builtin_amdgcn_raw_buffer_load_b64(rs_pw, wo1 + ro, 0, 0));
+        dacc[0][0] = MM::mma(x0, w0, dacc[0][0]);
+        dacc[0][1] = MM::mma(x0, w1, dacc[0][1]);
+        dacc[1][0] = MM::mma(x1, w0, dacc[1][0]);
+        dacc[1][1] = MM::mma(x1, w1, dacc[1][1]);
+      }
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          float d[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<TI>(dacc[pb][cb][e]));
+          char* rp = rowbuf + (16 * cb + i16) * PL::kStride + (16 * pb + q4) * 8;
+          reinterpret_cast<float2*>(rp)[0] = make_float2(d[0], d[1]);
+          reinterpret_cast<float2*>(rp + 16)[0] = make_float2(d[2], d[3]);
+        }
+      wave_lds_sync();
+    }
     uint4 ucur[kNV];
     auto stage = [&](auto masked) __attribute__((always_inline)) {
 #pragma unroll
@@ -134,9 +186,25 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
         char* dst = rowbuf + (j / kVPR) * PL::kStride + (j % kVPR) * VI * 8;
         ucur[k] = pu[k];
         const bool vok = !decltype(masked)::value || l0 + (j % kVPR) * VI < L_;
+        float dv[VI];
+#pragma unroll
+        for (int q = 0; q < VI / 2; ++q) {
+          if constexpr (kPD) {
+            const float2 d2 = reinterpret_cast<const float2*>(dst)[2 * q];
+            dv[2 * q] = d2.x;
+            dv[2 * q + 1] = d2.y;
+          } else {
+            dv[2 * q] = elem_f<TI>(pd[k], 2 * q);
+            dv[2 * q + 1] = elem_f<TI>(pd[k], 2 * q + 1);
+          }
+        }
+        if (kPD && a.delta_out) {   // the formed delta for the backward (rows / positions past the end dropped)
+          const uint32_t ob = ((j / kVPR) < nrows && l0 + (j % kVPR) * VI < L_) ? 0u : 0x80000000u;
+          buf_st16(rs_d, voff(k, a.dt_ds, l0) | ob, pack_f<TI>(dv));
+        }
 #pragma unroll
         for (int q = 0; q < VI / 2; ++q) {   // two positions per packed op
-          const f32x2 dr = f32x2{elem_f<TI>(pd[k], 2 * q), elem_f<TI>(pd[k], 2 * q + 1)} + biasv[k];
+          const f32x2 dr = f32x2{dv[2 * q], dv[2 * q + 1]} + biasv[k];
           f32x2 dt = kSP ? softplus2_log1p(dr) : dr;
           f32x2 du = dt * f32x2{elem_f<TI>(pu[k], 2 * q), elem_f<TI>(pu[k], 2 * q + 1)};
           if constexpr (decltype(masked)::value) {   // u past L may be anything (stride padding): mask du too
@@ -283,10 +351,14 @@ static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   a.nblk = (H + kPCh - 1) / kPCh;
   a.total_blocks = a.batch * a.n_groups * a.nblk;
   const size_t lds = (size_t)PairLayout<TI>::kRowBytes + PairLayout<TI>::kBCBytes;
-  if (a.softplus)
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
-  else
-    hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW>), dim3(a.total_blocks), dim3(64), lds, s, a);
+  const dim3 grid(a.total_blocks), block(64);
+  if (a.dpw) {
+    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, true>), grid, block, lds, s, a);
+  } else {
+    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, false>), grid, block, lds, s, a);
+  }
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
   return MC_OK;

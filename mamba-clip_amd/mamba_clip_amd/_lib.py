@@ -35,6 +35,9 @@ class ScanFwdParams(ctypes.Structure):
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
         ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
         ("reverse_groups", c_i32), ("u_groups", c_i32),
+        ("delta_proj_x", c_vp), ("delta_proj_w", c_vp), ("delta_rank", c_i32),
+        ("dpx_batch_stride", c_i64), ("dpx_token_stride", c_i64), ("dpw_dim_stride", c_i64),
+        ("delta_out", c_vp),
     ]
 
 
@@ -59,6 +62,8 @@ class ScanBwdParams(ctypes.Structure):
         ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
         ("out_y", c_vp), ("out_y_batch_stride", c_i64), ("out_y_dim_stride", c_i64),
         ("reverse_groups", c_i32), ("u_groups", c_i32),
+        ("delta_proj_x", c_vp), ("delta_proj_w", c_vp), ("delta_rank", c_i32),
+        ("dpx_batch_stride", c_i64), ("dpx_token_stride", c_i64), ("dpw_dim_stride", c_i64),
     ]
 
 

@@ -29,8 +29,8 @@ import torch.nn.functional as F
 
 from .ops import (GradSlab, add_layernorm, add_rmsnorm, causal_conv1d, fc1_gelu, linear_sk, patch_im2col, qkv_proj,
                   split_rows, wleft_mm)
-from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, SelectiveScanFn, grouped_scan_fn,
-                                       selective_scan_fn)
+from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
+                                       grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
 
 # ============================================================================ Mamba text tower
@@ -77,6 +77,7 @@ class MambaMixer(nn.Module):
         self.D = nn.Parameter(torch.ones(self.d_inner))
         self.D._no_weight_decay = True
         self.out_proj = nn.Linear(self.d_inner, d_model, bias=False)
+        self.fuse_dt_proj = True   # dt_proj inside the scan where the shapes allow (ProjectedScanFn)
 
     def forward(self, hidden):  # (B, L, d_model) contiguous
         Bsz, L, dm = hidden.shape
@@ -92,14 +93,25 @@ class MambaMixer(nn.Module):
         x = x.view(di, Bsz, L).transpose(0, 1)                                # (B, di, L) channel-major
         z = z.view(di, Bsz, L).transpose(0, 1)
         x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True, dx_slab=slab)
-        x_dbl = wleft_mm(self.x_proj.weight, x.transpose(0, 1).reshape(di, Bsz * L))   # (R+2N, B*L)
-        dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
-        delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
-        Bm = Bm.view(N, Bsz, L).transpose(0, 1)                               # (B, N, L)
-        Cm = Cm.view(N, Bsz, L).transpose(0, 1)
+        x_cm = x.transpose(0, 1).reshape(di, Bsz * L)                          # view
         A = -torch.exp(self.A_log.float())
-        y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(),
-                       (slab, di) if slab is not None else None)
+        dz = (slab, di) if slab is not None else None
+        if self.fuse_dt_proj and projected_scan_ok(x, R, N):
+            # dt_proj inside the scan (ProjectedScanFn): x_proj's dt rows come out token-major,
+            # (B*L, R), the scan kernel forms delta per chunk on MFMA; B / C stay channel-major
+            dt_raw = linear_sk(x_cm.t(), self.x_proj.weight[:R])              # (B*L, R)
+            BC = wleft_mm(self.x_proj.weight[R:], x_cm)                       # (2N, B*L)
+            Bm = BC[:N].view(N, Bsz, L).transpose(0, 1)
+            Cm = BC[N:].view(N, Bsz, L).transpose(0, 1)
+            y = ProjectedScanFn.apply(x, dt_raw, self.dt_proj.weight, A, Bm, Cm, self.D.float(), z,
+                                      self.dt_proj.bias.float(), True, dz)
+        else:
+            x_dbl = wleft_mm(self.x_proj.weight, x_cm)                         # (R+2N, B*L)
+            dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
+            delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
+            Bm = Bm.view(N, Bsz, L).transpose(0, 1)                           # (B, N, L)
+            Cm = Cm.view(N, Bsz, L).transpose(0, 1)
+            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz)
         y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
         out = linear_sk(y2.t(), self.out_proj.weight)                          # (B*L, d_model)
         return out.view(Bsz, L, dm)

@@ -57,7 +57,7 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
 
 
 def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False,
-             dirs=None):
+             dirs=None, proj=None):
     """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None[, out_y]).
 
     ``dirs=(reverse_groups, u_groups)``: grouped directions (include/mc_scan.h):
@@ -67,9 +67,14 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     forward returns it as ``out`` next to ``out_z``.  Training does not need it:
     the backward recomputes y from the chunk states (saving it measured slower:
     +1.6 GB of forward writes at C4 for less backward work).
+
+    ``proj=(dpx, dpw, delta_out)``: projected delta (include/mc_scan.h) -- delta is
+    None and the kernel forms delta[b, d, l] = dpw[d] . dpx[b, l] itself; dpx is
+    (batch, L, R) with unit stride along R, dpw (dim, R); ``delta_out`` (nullable,
+    u's layout) receives the formed delta for the backward.
     """
     lib = _lib.load()
-    batch, dim, L = delta.shape
+    batch, dim, L = (delta if delta is not None else u).shape
     dstate = A.shape[1]
     G = B.shape[1]
     # same (dense) layout as u: channel-major callers stay channel-major
@@ -84,15 +89,23 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     p.itype, p.wtype = _lib.dtype_code(u.dtype), _lib.dtype_code(B.dtype)
     p.delta_softplus = int(bool(delta_softplus))
     p.u_batch_stride, p.u_dim_stride = u.stride(0), u.stride(1)
-    p.delta_batch_stride, p.delta_dim_stride = delta.stride(0), delta.stride(1)
+    if delta is not None:
+        p.delta_batch_stride, p.delta_dim_stride = delta.stride(0), delta.stride(1)
     if z is not None:
         p.z_batch_stride, p.z_dim_stride = z.stride(0), z.stride(1)
     p.out_batch_stride, p.out_dim_stride = out.stride(0), out.stride(1)
     p.B_batch_stride, p.B_group_stride, p.B_dstate_stride = B.stride(0), B.stride(1), B.stride(2)
     p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
-    p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()
+    p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), _lib.ptr(delta), A.data_ptr(), B.data_ptr(), C.data_ptr()
     p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
     p.out, p.chunk_states, p.last_state = out.data_ptr(), _lib.ptr(states), _lib.ptr(last)
+    if proj is not None:
+        dpx, dpw, delta_out = proj
+        p.delta_proj_x, p.delta_proj_w, p.delta_rank = dpx.data_ptr(), dpw.data_ptr(), dpw.shape[1]
+        p.dpx_batch_stride, p.dpx_token_stride, p.dpw_dim_stride = dpx.stride(0), dpx.stride(1), dpw.stride(0)
+        if delta_out is not None:
+            p.delta_out = delta_out.data_ptr()
+            p.delta_batch_stride, p.delta_dim_stride = delta_out.stride(0), delta_out.stride(1)
     ws_bytes = lib.mc_scan_fwd_workspace_bytes(batch, L, dstate, G)
     ws = torch.empty(max(ws_bytes, 1), device=u.device, dtype=torch.uint8)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
@@ -109,10 +122,12 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None, proj=None):
     """Run mc_scan_bwd.  With ``dirs``, du comes back per group, (B, dim, L): the caller sums the
-    groups that share a u block."""
+    groups that share a u block.  ``proj=(dpx, dpw)``: projected delta (delta None), as scan_fwd."""
     lib = _lib.load()
+    if delta is None:
+        delta = u   # shape / layout template only: with proj the kernel re-forms delta, never reads it
     batch, dim, L = delta.shape
     dstate = A.shape[1]
     G = B.shape[1]
@@ -142,9 +157,14 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
         p.dz_batch_stride, p.dz_dim_stride = dz.stride(0), dz.stride(1)
     p.B_batch_stride, p.B_group_stride, p.B_dstate_stride = B.stride(0), B.stride(1), B.stride(2)
     p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
-    p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), delta.data_ptr(), A.data_ptr(), B.data_ptr(), C.data_ptr()
+    p.u, p.delta, p.A, p.B, p.C = (u.data_ptr(), 0 if proj is not None else delta.data_ptr(), A.data_ptr(),
+                                   B.data_ptr(), C.data_ptr())
     p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
     p.dout, p.chunk_states = dout.data_ptr(), states.data_ptr()
+    if proj is not None:
+        dpx, dpw = proj
+        p.delta_proj_x, p.delta_proj_w, p.delta_rank = dpx.data_ptr(), dpw.data_ptr(), dpw.shape[1]
+        p.dpx_batch_stride, p.dpx_token_stride, p.dpw_dim_stride = dpx.stride(0), dpx.stride(1), dpw.stride(0)
     p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
     p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
@@ -199,6 +219,75 @@ class SelectiveScanFn(torch.autograd.Function):
                 dz,
                 dbias.to(b_dt) if dbias is not None else None,
                 None, None, None)
+
+
+class ProjectedScanFn(torch.autograd.Function):
+    """The Mamba mixer's dt_proj + selective scan as one op (upstream mamba_inner_fn's fusion of
+    the delta projection; reference model.py:519-528, 630-647):
+
+        delta = dt_proj.weight @ dt_raw   (per token, rank R)
+        out   = selective_scan(u, delta, A, B, C, D, z, delta_bias, softplus)
+
+    ``dt_raw`` arrives token-major, (batch * L, R); both scan kernels form delta per chunk on the
+    matrix cores (the ``delta_proj_*`` fields of mc_scan.h), so the (batch, dim, L) delta never
+    touches HBM: no dt_proj GEMM output, no forward or backward read of it.  The backward's ddelta
+    then gives dt_raw's and the weight's gradients as GEMMs.
+    """
+
+    @staticmethod
+    def forward(ctx, u, dt_raw, weight, A, B, C, D, z, delta_bias, delta_softplus, dz_slab=None):
+        batch, dim, L = u.shape
+        R = weight.shape[1]
+        w = weight.to(u.dtype).contiguous()
+        dpx = dt_raw.view(batch, L, R)
+        squeeze_B, squeeze_C = B.dim() == 3, C.dim() == 3
+        B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
+        A32 = A.float().contiguous()
+        D32 = D.float().contiguous() if D is not None else None
+        bias32 = delta_bias.float().contiguous() if delta_bias is not None else None
+        _check_inputs(u, u, A32, B, C, D32, z, bias32)
+        need_grad = any(ctx.needs_input_grad[:9])
+        out, states, _ = scan_fwd(u, None, A32, B, C, D32, z, bias32, delta_softplus,
+                                  want_states=need_grad, want_last=False, proj=(dpx, w, None))
+        if need_grad:
+            ctx.save_for_backward(u, A32, B, C, D32, z, bias32, states, dt_raw, w)
+        ctx.delta_softplus = delta_softplus
+        ctx.squeeze = (squeeze_B, squeeze_C)
+        ctx.dtypes = (weight.dtype, A.dtype, D.dtype if D is not None else None,
+                      delta_bias.dtype if delta_bias is not None else None)
+        ctx.dz_slab = dz_slab
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, A32, B, C, D32, z, bias32, states, dt_raw, w = ctx.saved_tensors
+        dz_out = None
+        if ctx.dz_slab is not None and z is not None:
+            slab, r0 = ctx.dz_slab
+            dz_out = slab.block(r0, r0 + z.shape[1], z.shape[0])
+        batch, dim, L = u.shape
+        du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, None, A32, B, C, D32, z, bias32, ctx.delta_softplus,
+                                                         dout, states, dz_out=dz_out,
+                                                         proj=(dt_raw.view(batch, L, w.shape[1]), w))
+        # ddelta has u's layout; as a (dim, batch * L) matrix it is channel-major rows
+        g = ddelta.transpose(0, 1).reshape(dim, batch * L)
+        from .ops import wgrad
+        d_raw = torch.mm(g.t(), w) if ctx.needs_input_grad[1] else None
+        d_w = wgrad(g, dt_raw) if ctx.needs_input_grad[2] else None
+        if ctx.squeeze[0]:
+            dB = dB.squeeze(1)
+        if ctx.squeeze[1]:
+            dC = dC.squeeze(1)
+        w_dt, a_dt, d_dt, b_dt = ctx.dtypes
+        return (du, d_raw, d_w.to(w_dt) if d_w is not None else None, dA.to(a_dt), dB, dC,
+                dD.to(d_dt) if dD is not None else None, dz,
+                dbias.to(b_dt) if dbias is not None else None, None, None)
+
+
+def projected_scan_ok(u, rank, dstate):
+    """Shapes the projected-delta scan takes (the pair kernel's: mc_scan.h)."""
+    return (u.is_cuda and u.dtype in (torch.bfloat16, torch.float16) and dstate == 16 and u.shape[2] % 8 == 0
+            and rank % 16 == 0 and 16 <= rank <= 256)
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,

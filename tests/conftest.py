@@ -31,3 +31,13 @@ def golden_meta(name):
 @pytest.fixture
 def golden():
     return load_golden
+
+
+@pytest.fixture(autouse=True)
+def _restore_tf32_flags():
+    """init_device (utils/dist_utils.py, as the reference's) turns TF32 on process-wide; tests that
+    run it (CLI, train) must not change the precision of fp32 reference matmuls in later tests."""
+    import torch
+    saved = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
+    yield
+    torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = saved

@@ -336,3 +336,63 @@ def test_scan_fwd_pair_masked_chunk_ignores_nan_padding():
     assert torch.equal(out, out0) and torch.equal(last, last0)
     _, ref_last = selective_scan_ref(**x, delta_softplus=True, return_last_state=True, compute_dtype=torch.float64)
     assert_scan_close(last, ref_last, torch.float32, "last_state")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,L,dim", [(16, 64, 64), (48, 80, 80), (96, 1000, 96)])
+def test_scan_projected_delta_matches_explicit_delta(dt, R, L, dim):
+    """mc_scan_fwd's projected delta (dt_proj inside the scan): the formed delta equals the GEMM's
+    (dim x R) . (R x tokens) rounded to the activation dtype within one ulp (fp32 sums in another
+    order), and given that delta the scan output and saved chunk states are bit-identical to the
+    explicit-delta call.  dim 80: a partial 32-channel block; L 1000: a masked last chunk."""
+    from mamba_clip_amd.selective_scan_interface import scan_fwd
+    torch.manual_seed(R + L)
+    batch, N = 2, 16
+    u = torch.randn(dim, batch * L, device=DEV).to(dt).view(dim, batch, L).transpose(0, 1)   # channel-major
+    z = torch.randn(dim, batch * L, device=DEV).to(dt).view(dim, batch, L).transpose(0, 1)
+    dpx = (0.5 * torch.randn(batch * L, R, device=DEV)).to(dt)
+    W = (torch.randn(dim, R, device=DEV) * R ** -0.5).to(dt)
+    A = -torch.rand(dim, N, device=DEV) - 0.2
+    Bm = torch.randn(batch, N, L, device=DEV).to(dt).unsqueeze(1)
+    Cm = torch.randn(batch, N, L, device=DEV).to(dt).unsqueeze(1)
+    D = torch.randn(dim, device=DEV)
+    bias = torch.randn(dim, device=DEV) * 0.5 - 2.0
+    ref = (W.double() @ dpx.double().t()).to(dt).view(dim, batch, L).transpose(0, 1)
+    delta_out = torch.empty_like(u)
+    out_p, st_p, _ = scan_fwd(u, None, A, Bm, Cm, D, z, bias, True, want_states=True, want_last=False,
+                              proj=(dpx.view(batch, L, R), W, delta_out))
+    ulp = ref.float().abs() * (2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10) + 1e-6
+    assert ((delta_out.float() - ref.float()).abs() <= ulp).all()
+    out_e, st_e, _ = scan_fwd(u, delta_out, A, Bm, Cm, D, z, bias, True, want_states=True, want_last=False)
+    assert torch.equal(out_p, out_e)
+    assert torch.equal(st_p, st_e)
+    # inference form: no delta written
+    out_i, _, _ = scan_fwd(u, None, A, Bm, Cm, D, z, bias, True, want_states=False, want_last=False,
+                           proj=(dpx.view(batch, L, R), W, None))
+    assert torch.equal(out_i, out_p)
+    # backward: re-forming delta per chunk gives every gradient bit-identical to reading delta_out
+    from mamba_clip_amd.selective_scan_interface import scan_bwd
+    dout = torch.randn(dim, batch * L, device=DEV).to(dt).view(dim, batch, L).transpose(0, 1)
+    g_p = scan_bwd(u, None, A, Bm, Cm, D, z, bias, True, dout, st_p, proj=(dpx.view(batch, L, R), W))
+    g_e = scan_bwd(u, delta_out, A, Bm, Cm, D, z, bias, True, dout, st_e)
+    for name, a, b in zip(("du", "ddelta", "dA", "dB", "dC", "dD", "dz", "dbias"), g_p, g_e):
+        assert torch.equal(a, b), name
+
+
+def test_scan_projected_delta_rejects_bad_shapes():
+    from mamba_clip_amd.selective_scan_interface import scan_fwd
+    dt = torch.bfloat16
+    u = torch.randn(1, 32, 64, device=DEV).to(dt)
+    A = -torch.rand(32, 16, device=DEV)
+    Bm = torch.randn(1, 1, 16, 64, device=DEV).to(dt)
+    for R in (8, 24):   # rank must be a multiple of 16
+        dpx = torch.randn(1, 64, R, device=DEV).to(dt)
+        W = torch.randn(32, R, device=DEV).to(dt)
+        with pytest.raises(RuntimeError, match="delta_rank"):
+            scan_fwd(u, None, A, Bm, Bm, None, None, None, True, False, False, proj=(dpx, W, None))
+    dpx = torch.randn(1, 64, 16, device=DEV).to(dt)
+    W = torch.randn(32, 16, device=DEV).to(dt)
+    u60 = torch.randn(1, 32, 60, device=DEV).to(dt)   # seqlen % 8 != 0: not a pair-kernel shape
+    with pytest.raises(RuntimeError, match="pair kernel"):
+        scan_fwd(u60, None, A, Bm[..., :60].contiguous(), Bm[..., :60].contiguous(), None, None, None, True, False,
+                 False, proj=(dpx[:, :60], W, None))
