@@ -77,7 +77,10 @@ class MambaMixer(nn.Module):
         self.D = nn.Parameter(torch.ones(self.d_inner))
         self.D._no_weight_decay = True
         self.out_proj = nn.Linear(self.d_inner, d_model, bias=False)
-        self.fuse_dt_proj = True   # dt_proj inside the scan where the shapes allow (ProjectedScanFn)
+        # dt_proj inside the scan (ProjectedScanFn) where the shapes allow.  Off by default: the scan
+        # kernels are VALU-bound, so forming delta on their MFMAs costs more than the delta stream it
+        # saves (C2 step 88.4 vs 86.5 ms on one box, profiles/r03/c2_ab_fuse_dt_proj.txt)
+        self.fuse_dt_proj = False
 
     def forward(self, hidden):  # (B, L, d_model) contiguous
         Bsz, L, dm = hidden.shape
