@@ -100,6 +100,27 @@ class QkvPackParams(ctypes.Structure):
     ]
 
 
+class AttnFwdParams(ctypes.Structure):
+    """Mirror of ``mc_attn_fwd_params`` (include/mc_attn.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("heads", c_i32), ("seqlen", c_i32), ("head_dim", c_i32), ("dtype", c_i32),
+        ("scale", ctypes.c_float),
+        ("q", c_vp), ("k", c_vp), ("v", c_vp), ("q_bs", c_i64), ("q_ns", c_i64), ("q_hs", c_i64),
+        ("o", c_vp), ("o_bs", c_i64), ("o_ns", c_i64), ("o_hs", c_i64), ("lse", c_fp),
+    ]
+
+
+class AttnBwdParams(ctypes.Structure):
+    """Mirror of ``mc_attn_bwd_params`` (include/mc_attn.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("heads", c_i32), ("seqlen", c_i32), ("head_dim", c_i32), ("dtype", c_i32),
+        ("scale", ctypes.c_float),
+        ("q", c_vp), ("k", c_vp), ("v", c_vp), ("q_bs", c_i64), ("q_ns", c_i64), ("q_hs", c_i64),
+        ("o", c_vp), ("dout", c_vp), ("o_bs", c_i64), ("o_ns", c_i64), ("o_hs", c_i64), ("lse", c_fp),
+        ("dq", c_vp), ("dk", c_vp), ("dv", c_vp), ("dq_bs", c_i64), ("dq_ns", c_i64), ("dq_hs", c_i64),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -144,6 +165,8 @@ SYMBOLS = {
                                    ctypes.c_size_t, c_vp]),
     "mc_qkv_grad_pack": (ctypes.c_int, [ctypes.POINTER(QkvPackParams), c_vp]),
     "mc_stream_copy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
+    "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),
 }
 
 _lib = None

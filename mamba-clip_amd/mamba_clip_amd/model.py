@@ -27,8 +27,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import (GradSlab, add_layernorm, add_rmsnorm, causal_conv1d, fc1_gelu, linear_sk, patch_im2col, qkv_proj,
-                  split_rows, wleft_mm)
+from .ops import (GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d, fc1_gelu,
+                  linear_sk, packed_attention, patch_im2col, qkv_proj, split_rows, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
@@ -215,9 +215,16 @@ class Attention(nn.Module):
         self.heads = heads
         self.qkv = nn.Linear(dim, 3 * dim, bias=True)
         self.proj = nn.Linear(dim, dim)
+        self.fused_attention = True   # mc_attn_fwd/bwd where supported (bf16/f16, head_dim 64, N <= 256)
 
     def forward(self, x):
         Bsz, N, C = x.shape
+        if self.fused_attention and x.is_cuda and attn_supported(N, C // self.heads, _compute_dtype(x)):
+            # packed qkv projection -> fused attention kernel (ops.PackedAttentionFn: the whole
+            # sequence of a head in LDS) -> output projection; o is already (B, N, C) and the
+            # backward writes dq / dk / dv into the packed projection gradient
+            qkv = linear_sk(x, self.qkv.weight, self.qkv.bias)
+            return linear_sk(packed_attention(qkv, self.heads), self.proj.weight, self.proj.bias)
         # unbind (not index) the q/k/v slices: its backward stacks the three
         # gradients in one write instead of zero-filling and accumulating a
         # (3, B, H, N, D) buffer three times and copying it contiguous again

@@ -781,3 +781,68 @@ class QKVProjFn(torch.autograd.Function):
 
 def qkv_proj(x, weight, bias, heads):
     return QKVProjFn.apply(x, weight, bias, heads)
+
+
+# ---------------------------------------------------------------------------- fused short-sequence attention (mc_attn.h)
+def attn_supported(seqlen, head_dim, dtype):
+    return head_dim == 64 and 1 <= seqlen <= 256 and dtype in (torch.bfloat16, torch.float16)
+
+
+class PackedAttentionFn(torch.autograd.Function):
+    """o = softmax(q k^T / sqrt(D)) v per head, for q / k / v the three C-wide slices of a packed
+    (B, N, 3C) projection output (timm Attention's qkv Linear), o as (B, N, C) -- the layout
+    the output projection reads.  Forward mc_attn_fwd, backward mc_attn_bwd writing dq / dk / dv
+    straight into the packed (B, N, 3C) gradient of the projection output (no stack, no copy)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        Bsz, N, C3 = qkv.shape
+        C = C3 // 3
+        D = C // heads
+        if not (qkv.is_cuda and attn_supported(N, D, qkv.dtype)):
+            raise RuntimeError(f"packed_attention: unsupported (device {qkv.device}, N {N}, head_dim {D}, "
+                               f"{qkv.dtype}); bf16/f16 on the GPU, head_dim 64, N <= 256")
+        lib = _lib.load()
+        y = _hip_rows(qkv.reshape(Bsz * N, C3), 8, "packed_attention").view(Bsz, N, C3)
+        o = torch.empty(Bsz, N, C, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(Bsz, heads, N, device=qkv.device, dtype=torch.float32)
+        p = _lib.AttnFwdParams()
+        p.batch, p.heads, p.seqlen, p.head_dim, p.dtype = Bsz, heads, N, D, _lib.dtype_code(qkv.dtype)
+        p.scale = D ** -0.5
+        es = y.element_size()
+        p.q, p.k, p.v = y.data_ptr(), y.data_ptr() + C * es, y.data_ptr() + 2 * C * es
+        p.q_bs, p.q_ns, p.q_hs = y.stride(0), y.stride(1), D
+        p.o, p.o_bs, p.o_ns, p.o_hs = o.data_ptr(), o.stride(0), o.stride(1), D
+        p.lse = lse.data_ptr()
+        _lib.check(lib.mc_attn_fwd(p, _lib.stream_handle(qkv.device)), "mc_attn_fwd")
+        ctx.save_for_backward(y, o, lse)
+        ctx.heads = heads
+        return o
+
+    @staticmethod
+    def backward(ctx, go):
+        y, o, lse = ctx.saved_tensors
+        Bsz, N, C3 = y.shape
+        C = C3 // 3
+        D = C // ctx.heads
+        lib = _lib.load()
+        g = _hip_rows(go.to(o.dtype).reshape(Bsz * N, C), 8, "packed_attention backward").view(Bsz, N, C)
+        dy = torch.empty_like(y)
+        p = _lib.AttnBwdParams()
+        p.batch, p.heads, p.seqlen, p.head_dim, p.dtype = Bsz, ctx.heads, N, D, _lib.dtype_code(y.dtype)
+        p.scale = D ** -0.5
+        es = y.element_size()
+        p.q, p.k, p.v = y.data_ptr(), y.data_ptr() + C * es, y.data_ptr() + 2 * C * es
+        p.q_bs, p.q_ns, p.q_hs = y.stride(0), y.stride(1), D
+        if g.stride() != o.stride():
+            raise RuntimeError("packed_attention backward: dout and o layouts differ")
+        p.o, p.dout, p.o_bs, p.o_ns, p.o_hs = o.data_ptr(), g.data_ptr(), o.stride(0), o.stride(1), D
+        p.lse = lse.data_ptr()
+        p.dq, p.dk, p.dv = dy.data_ptr(), dy.data_ptr() + C * es, dy.data_ptr() + 2 * C * es
+        p.dq_bs, p.dq_ns, p.dq_hs = dy.stride(0), dy.stride(1), D
+        _lib.check(lib.mc_attn_bwd(p, _lib.stream_handle(y.device)), "mc_attn_bwd")
+        return dy, None
+
+
+def packed_attention(qkv, heads):
+    return PackedAttentionFn.apply(qkv, heads)

@@ -88,15 +88,40 @@ def test_fused_ce_validation_without_launch():
     assert lib.mc_ce_fused_fwd_workspace_bytes(0, 5, 1) == 0
 
 
+def test_attention_validation_without_launch():
+    """mc_attn_fwd / _bwd reject unsupported shapes, dtypes and layouts on the host."""
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    p = _lib.AttnFwdParams()
+    p.batch, p.heads, p.seqlen, p.head_dim, p.dtype = 2, 12, 197, 128, _lib.MC_DTYPE_BF16
+    assert lib.mc_attn_fwd(ctypes.byref(p), None) == -3 and b"head_dim" in lib.mc_last_error()
+    p.head_dim, p.seqlen = 64, 257
+    assert lib.mc_attn_fwd(ctypes.byref(p), None) == -3
+    p.seqlen, p.dtype = 197, _lib.MC_DTYPE_F32
+    assert lib.mc_attn_fwd(ctypes.byref(p), None) == -2
+    p.dtype = _lib.MC_DTYPE_BF16
+    assert lib.mc_attn_fwd(ctypes.byref(p), None) == -1          # null tensors
+    p.q = p.k = p.v = p.o = p.lse = 4096
+    p.q_bs, p.q_ns, p.q_hs, p.o_bs, p.o_ns, p.o_hs = 197 * 2304, 2304, 64, 197 * 768, 770, 64   # o_ns % 8 != 0
+    assert lib.mc_attn_fwd(ctypes.byref(p), None) == -1 and b"aligned" in lib.mc_last_error()
+    b = _lib.AttnBwdParams()
+    b.batch, b.heads, b.seqlen, b.head_dim, b.dtype = 2, 12, 197, 64, _lib.MC_DTYPE_BF16
+    assert lib.mc_attn_bwd(ctypes.byref(b), None) == -1
+
+
 @pytest.mark.parametrize("cname,pyname", [("mc_scan_fwd_params", "ScanFwdParams"),
                                           ("mc_scan_bwd_params", "ScanBwdParams"),
                                           ("mc_gemm_nt_params", "GemmNTParams"),
-                                          ("mc_ce_fused_params", "CEFusedParams")])
+                                          ("mc_ce_fused_params", "CEFusedParams"),
+                                          ("mc_qkv_pack_params", "QkvPackParams"),
+                                          ("mc_attn_fwd_params", "AttnFwdParams"),
+                                          ("mc_attn_bwd_params", "AttnBwdParams")])
 def test_struct_layout_matches_header(cname, pyname):
     from mamba_clip_amd import _lib
     cls = getattr(_lib, pyname)
     fields = [f for f, _ in cls._fields_]
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', '#include "mc_contrastive.h"',
+           '#include "mc_ops.h"', '#include "mc_attn.h"',
            "int main(void){",
            f'printf("size %zu\\n", sizeof({cname}));']
     src += [f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields]
