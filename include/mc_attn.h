@@ -55,6 +55,9 @@ typedef struct {
   const float* lse;                   /* from mc_attn_fwd */
   void* dq; void* dk; void* dv;
   int64_t dq_bs, dq_ns, dq_hs;        /* shared by dq, dk, dv */
+  float* dsum;                        /* (batch, 3, heads, head_dim) fp32, nullable: per-batch sums over the
+                                         sequence of dq | dk | dv as stored -- summed over the batch, the bias
+                                         gradient of a packed qkv projection (no second pass over dq / dk / dv) */
 } mc_attn_bwd_params;
 
 /* dq, dk, dv of the above given dout (recomputes the probabilities from q, k and lse). */

@@ -115,6 +115,20 @@ int mc_qkv_grad_pack(const mc_qkv_pack_params* p, void* stream);
  * HBM streaming rate next to the 8 TB/s spec.  16-B aligned, nbytes % 16 == 0. */
 int mc_stream_copy(const void* src, void* dst, size_t nbytes, void* stream);
 
+/* mc_cast_f32_many: dst_base[c.dst_off + i] = (dtype) c.src[i], i < c.n, for every chunk c, in ONE
+ * launch (RNE: the bits of torch's .to(bfloat16 / float16)).  The towers' projection weights are
+ * cast once per forward instead of one cast kernel per weight and use (~230 launches per C2 step).
+ * chunks: DEVICE array of n_chunks entries, each at most MC_CAST_CHUNK elements; the table holds
+ * destination OFFSETS (elements) so one table serves a fresh dst_base every forward.  dst_dtype
+ * bf16 or f16.  Chunks with 16-B aligned src / dst and n % 8 == 0 move as 16-B vectors. */
+#define MC_CAST_CHUNK 16384
+typedef struct {
+  const float* src;
+  int64_t dst_off;
+  int64_t n;
+} mc_cast_chunk;
+int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, void* dst_base, int32_t dst_dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,7 @@ namespace attn {
 
 constexpr int kD = 64;            // head dim
 constexpr int kRowB = kD * 2;     // bytes per 16-bit row
-constexpr int kFwdWaves = 4;
+constexpr int kFwdWaves = 8;   // one 32-query block per wave (N <= 256); two workgroups per CU
 constexpr int kBwdWaves = 8;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -86,12 +86,32 @@ __device__ __forceinline__ float swap_sum(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// Sum over the 32 lanes of this lane's half (xor butterfly: DPP inside a 16-lane row, a swizzle
+// across the two rows).
+template <int kCtrl>
+__device__ __forceinline__ float dpp_xor(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row_xor4(float v) {   // banks 0 / 2 take lane + 4, banks 1 / 3 lane - 4
+  const int iv = __float_as_int(v);
+  const int lo = __builtin_amdgcn_update_dpp(iv, iv, 0x104, 0xF, 0x5, false);
+  return __int_as_float(__builtin_amdgcn_update_dpp(lo, iv, 0x114, 0xF, 0xA, false));
+}
+__device__ __forceinline__ float sum_half32(float v) {
+  v += dpp_xor<0xB1>(v);    // quad_perm [1, 0, 3, 2]: lane ^ 1
+  v += dpp_xor<0x4E>(v);    // quad_perm [2, 3, 0, 1]: lane ^ 2
+  v += row_xor4(v);
+  v += dpp_xor<0x128>(v);   // row_ror:8: lane ^ 8
+  return v + __shfl_xor(v, 16);
+}
+
 // Store a transposed accumulator pair (x0: d in [0, 32), x1: [32, 64); column = this lane's row
 // `row`, accumulator rows = d) as 16-B pieces: permlane32 swaps turn each lane's 4-element groups
 // into 8 consecutive d (T21).  rows >= nrows are dropped.
+// csum (LDS, 64 floats, nullable): the tile's column sums of the stored (rounded) values, rows < nrows.
 template <typename TI>
 __device__ __forceinline__ void store_rows(TI* base, int64_t ns, int row, int nrows, int lane, const f32x16& x0,
-                                           const f32x16& x1, float mul) {
+                                           const f32x16& x1, float mul, float* csum = nullptr) {
   const int hh = lane >> 5;
 #pragma unroll
   for (int db = 0; db < 2; ++db) {
@@ -106,9 +126,14 @@ __device__ __forceinline__ void store_rows(TI* base, int64_t ns, int row, int nr
         v[i] = __uint_as_float(r[0]) * mul;
         v[4 + i] = __uint_as_float(r[1]) * mul;
       }
-      if (row < nrows) {
-        const int d0 = db * 32 + 16 * m + 8 * hh;
-        *reinterpret_cast<uint4*>(base + (int64_t)row * ns + d0) = pack_f<TI>(v);
+      const int d0 = db * 32 + 16 * m + 8 * hh;
+      if (row < nrows) *reinterpret_cast<uint4*>(base + (int64_t)row * ns + d0) = pack_f<TI>(v);
+      if (csum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float sv = sum_half32(row < nrows ? to_f(from_f<TI>(v[e])) : 0.f);
+          if ((lane & 31) == 0) csum[d0 + e] = sv;
+        }
       }
     }
   }
@@ -139,37 +164,37 @@ __global__ __launch_bounds__(64 * kFwdWaves, 2) void attn_fwd_kernel(const FwdAr
   const TI* kg = reinterpret_cast<const TI*>(a.k) + off;
   const TI* vg = reinterpret_cast<const TI*>(a.v) + off;
 
-  // K / V images: all NT pieces per thread in flight at once (buffer loads: rows past N read 0)
+  // K / V images: every piece of a thread in flight at once (buffer loads: rows past N read 0)
+  constexpr int kPer = (Np * 8 + 64 * kFwdWaves - 1) / (64 * kFwdWaves);
   const uint32_t rng = (uint32_t)(((int64_t)(N - 1) * a.q_ns + kD) * (int64_t)sizeof(TI));
   const __amdgpu_buffer_rsrc_t rk = make_rsrc(kg, rng), rv = make_rsrc(vg, rng);
-  uint4 kr[NT], vr[NT];
+  uint4 kr[kPer], vr[kPer];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
+  for (int j = 0; j < kPer; ++j) {
     const int i = tid + 64 * kFwdWaves * j, r = i >> 3, c = i & 7;
     const uint32_t o = r < N ? (uint32_t)(r * a.q_ns + 8 * c) * (uint32_t)sizeof(TI) : 0x80000000u;
     kr[j] = buf_ld16(rk, o);
     vr[j] = buf_ld16(rv, o);
   }
-  auto load_q = [&](int qt, uint4 (&f)[4]) __attribute__((always_inline)) {
-    const TI* qrow = qg + (int64_t)min(qt * 32 + l32, N - 1) * a.q_ns;
+  // this wave's 32-query block (B operand: lane = query, 16-B chunks 2 s + hh of its row)
+  const int qt = wave;
+  const int q = qt * 32 + l32;
+  uint4 qf[4];
+  {
+    const TI* qrow = qg + (int64_t)min(q, N - 1) * a.q_ns;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = ld16(qrow + 16 * s + 8 * hh);
-  };
-  uint4 qn[4];
-  if (wave < NT) load_q(wave, qn);
+    for (int s = 0; s < 4; ++s) qf[s] = ld16(qrow + 16 * s + 8 * hh);
+  }
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
+  for (int j = 0; j < kPer; ++j) {
     const int i = tid + 64 * kFwdWaves * j, r = i >> 3, c = i & 7;
-    *reinterpret_cast<uint4*>(kimg + img_off(r, c)) = kr[j];
-    *reinterpret_cast<uint4*>(vimg + img_off(r, c)) = vr[j];
+    if (i < Np * 8) {
+      *reinterpret_cast<uint4*>(kimg + img_off(r, c)) = kr[j];
+      *reinterpret_cast<uint4*>(vimg + img_off(r, c)) = vr[j];
+    }
   }
   __syncthreads();
-
-  for (int qt = wave; qt < NT; qt += kFwdWaves) {
-    const int q = qt * 32 + l32;
-    uint4 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+  if (qt < NT) {
     // S^T tiles: rows = keys t*32 + (r & 3) + 8 (r >> 2) + 4 hh, column = this lane's query.
     // Two passes over the key tiles (the row max, then the probabilities and P V): recomputing
     // S costs 4 MFMAs per tile and keeps one tile of scores live instead of all NT (no spills).
@@ -193,7 +218,6 @@ __global__ __launch_bounds__(64 * kFwdWaves, 2) void attn_fwd_kernel(const FwdAr
     }
     m = swap_max(m);
     const float mc = m * a.c2;
-    if (qt + kFwdWaves < NT) load_q(qt + kFwdWaves, qn);   // the next block's Q, in flight during P V
     // O^T = V^T P^T: two 32-row d blocks, lane = query
     float l = 0.f;
     f32x16 o0 = {}, o1 = {};
@@ -231,6 +255,7 @@ struct BwdArgs {
   const float* lse;
   void* dq; void* dk; void* dv;
   int64_t d_bs, d_ns, d_hs;
+  float* dsum;   // (B, 3, H, 64) or null
 };
 
 template <typename TI, int NT>
@@ -245,6 +270,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
   char* gimg = smem + 3 * kImg;
   float* lse2 = reinterpret_cast<float*>(smem + 4 * kImg);   // lse * log2(e); +inf past N (P = 0)
   float* dlt = lse2 + Np;                                      // rowsum(dO o O)
+  float* csl = dlt + Np;                                       // [dq | dk | dv][wave][64] tile column sums
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hh = lane >> 5, l32 = lane & 31, g16 = 16 * ((lane >> 4) & 1);
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
@@ -300,24 +326,26 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
   }
   __syncthreads();
 
-  // ---- phase 1: wave = key tile; dV^T += dO^T P, dK^T += Q^T dS over the query blocks
+  // ---- phase 1: wave = key tile; dV^T += dO^T P, dK^T += Q^T dS over the query blocks.
+  // Software pipeline: the next block's S / dP MFMAs are issued before this block's four gradient
+  // MFMAs, so the next softmax (VALU) overlaps them; K / V fragments are re-read from LDS per
+  // block (registers for the pipelined accumulators instead).
   if (wave < NT) {
     const int kt = wave;
-    uint4 kf[4], vf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = row_chunk(kimg, kt * 32 + l32, 2 * s + hh);
-      vf[s] = row_chunk(vimg, kt * 32 + l32, 2 * s + hh);
-    }
-    f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
-#pragma unroll 1
-    for (int qt = 0; qt < NT; ++qt) {
-      f32x16 sa = {}, pa = {};
+    auto sdp = [&](int qt, f32x16& sa, f32x16& pa) __attribute__((always_inline)) {
+      sa = f32x16{};
+      pa = f32x16{};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sa = M::mma(row_chunk(qimg, qt * 32 + l32, 2 * s + hh), kf[s], sa);
-        pa = M::mma(row_chunk(gimg, qt * 32 + l32, 2 * s + hh), vf[s], pa);
+        sa = M::mma(row_chunk(qimg, qt * 32 + l32, 2 * s + hh), row_chunk(kimg, kt * 32 + l32, 2 * s + hh), sa);
+        pa = M::mma(row_chunk(gimg, qt * 32 + l32, 2 * s + hh), row_chunk(vimg, kt * 32 + l32, 2 * s + hh), pa);
       }
+    };
+    f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+    f32x16 sa, pa;
+    sdp(0, sa, pa);
+#pragma unroll 1
+    for (int qt = 0; qt < NT; ++qt) {
       // rows of this lane's accumulators: queries qt*32 + 8 j + 4 hh + i  (register 4 j + i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -330,9 +358,12 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
           pa[4 * j + i] = p * (pa[4 * j + i] - Dl[i]);
         }
       }
+      const uint4 pf0 = acc_frag<TI>(sa, 0), df0 = acc_frag<TI>(pa, 0);
+      const uint4 pf1 = acc_frag<TI>(sa, 1), df1 = acc_frag<TI>(pa, 1);
+      if (qt + 1 < NT) sdp(qt + 1, sa, pa);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const uint4 pf = acc_frag<TI>(sa, s2), df = acc_frag<TI>(pa, s2);
+        const uint4 pf = s2 ? pf1 : pf0, df = s2 ? df1 : df0;
         const int r0 = qt * 32 + 16 * s2 + 4 * hh;
         dv0 = M::mma(tr_chunk(gimg, r0, g16, lane), pf, dv0);
         dv1 = M::mma(tr_chunk(gimg, r0, 32 + g16, lane), pf, dv1);
@@ -341,11 +372,14 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
       }
     }
     const int64_t doff = (int64_t)b * a.d_bs + (int64_t)h * a.d_hs;
-    store_rows<TI>(reinterpret_cast<TI*>(a.dk) + doff, a.d_ns, kt * 32 + l32, N, lane, dk0, dk1, a.scale);
-    store_rows<TI>(reinterpret_cast<TI*>(a.dv) + doff, a.d_ns, kt * 32 + l32, N, lane, dv0, dv1, 1.f);
+    store_rows<TI>(reinterpret_cast<TI*>(a.dk) + doff, a.d_ns, kt * 32 + l32, N, lane, dk0, dk1, a.scale,
+                   a.dsum ? csl + (1 * kBwdWaves + wave) * kD : nullptr);
+    store_rows<TI>(reinterpret_cast<TI*>(a.dv) + doff, a.d_ns, kt * 32 + l32, N, lane, dv0, dv1, 1.f,
+                   a.dsum ? csl + (2 * kBwdWaves + wave) * kD : nullptr);
   }
 
-  // ---- phase 2: wave = query block; dQ^T += K^T dS^T over the key tiles (forward orientation)
+  // ---- phase 2: wave = query block; dQ^T += K^T dS^T over the key tiles (forward orientation),
+  // pipelined the same way
   if (wave < NT) {
     const int qt = wave, q = qt * 32 + l32;
     uint4 qf[4], gf[4];
@@ -355,35 +389,53 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
       gf[s] = row_chunk(gimg, q, 2 * s + hh);
     }
     const float L = lse2[q], Dl = dlt[q];
-    f32x16 dq0 = {}, dq1 = {};
-#pragma unroll 1
-    for (int kt = 0; kt < NT; ++kt) {
-      f32x16 sa = {}, pa = {};
+    auto sdp = [&](int kt, f32x16& sa, f32x16& pa) __attribute__((always_inline)) {
+      sa = f32x16{};
+      pa = f32x16{};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         sa = M::mma(row_chunk(kimg, kt * 32 + l32, 2 * s + hh), qf[s], sa);
         pa = M::mma(row_chunk(vimg, kt * 32 + l32, 2 * s + hh), gf[s], pa);
       }
+    };
+    f32x16 dq0 = {}, dq1 = {};
+    f32x16 sa, pa;
+    sdp(0, sa, pa);
+#pragma unroll 1
+    for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = fast_exp2(sa[r] * a.c2 - L);
         pa[r] = p * (pa[r] - Dl);
       }
+      const uint4 df0 = acc_frag<TI>(pa, 0), df1 = acc_frag<TI>(pa, 1);
+      if (kt + 1 < NT) sdp(kt + 1, sa, pa);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const uint4 df = acc_frag<TI>(pa, s2);
+        const uint4 df = s2 ? df1 : df0;
         const int r0 = kt * 32 + 16 * s2 + 4 * hh;
         dq0 = M::mma(tr_chunk(kimg, r0, g16, lane), df, dq0);
         dq1 = M::mma(tr_chunk(kimg, r0, 32 + g16, lane), df, dq1);
       }
     }
     const int64_t doff = (int64_t)b * a.d_bs + (int64_t)h * a.d_hs;
-    store_rows<TI>(reinterpret_cast<TI*>(a.dq) + doff, a.d_ns, q, N, lane, dq0, dq1, a.scale);
+    store_rows<TI>(reinterpret_cast<TI*>(a.dq) + doff, a.d_ns, q, N, lane, dq0, dq1, a.scale,
+                   a.dsum ? csl + wave * kD : nullptr);
+  }
+  if (a.dsum) {   // per-(batch, head) column sums, tiles in fixed order (deterministic)
+    __syncthreads();
+    if (tid < 3 * kD) {
+      const int o = tid / kD, d = tid % kD;
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT; ++w) acc += csl[(o * kBwdWaves + w) * kD + d];
+      a.dsum[(((int64_t)b * 3 + o) * a.H + h) * kD + d] = acc;
+    }
   }
 }
 
 size_t fwd_lds(int NT) { return (size_t)2 * NT * 32 * kRowB; }
-size_t bwd_lds(int NT) { return (size_t)4 * NT * 32 * kRowB + (size_t)2 * NT * 32 * 4; }
+size_t bwd_lds(int NT) { return (size_t)4 * NT * 32 * kRowB + (size_t)2 * NT * 32 * 4 + (size_t)3 * kBwdWaves * kD * 4; }
 
 template <typename TI, int NT>
 void launch_fwd_nt(const FwdArgs& a, hipStream_t s) {
@@ -478,6 +530,7 @@ extern "C" int mc_attn_bwd(const mc_attn_bwd_params* p, void* stream) {
   a.lse = p->lse;
   a.dq = p->dq; a.dk = p->dk; a.dv = p->dv;
   a.d_bs = p->dq_bs; a.d_ns = p->dq_ns; a.d_hs = p->dq_hs;
+  a.dsum = p->dsum;
   if (p->dtype == MC_DTYPE_BF16) attn::launch_bwd<bf16_t>(a, (hipStream_t)stream);
   else attn::launch_bwd<f16_t>(a, (hipStream_t)stream);
   const hipError_t e = hipGetLastError();

@@ -1046,3 +1046,38 @@ extern "C" int mc_stream_copy(const void* src, void* dst, size_t nbytes, void* s
                      reinterpret_cast<const u32x4_t*>(src), reinterpret_cast<u32x4_t*>(dst), n16);
   return check_launch("mc_stream_copy");
 }
+
+// ---------------------------------------------------------------------------- many fp32 -> 16-bit casts, one launch
+namespace {
+template <typename TO>
+__global__ __launch_bounds__(256) void cast_many_kernel(const mc_cast_chunk* __restrict__ chunks, TO* __restrict__ base) {
+  const mc_cast_chunk c = chunks[blockIdx.x];
+  TO* __restrict__ dst = base + c.dst_off;
+  const bool vec = ((reinterpret_cast<uintptr_t>(c.src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0 && (c.n & 7) == 0;
+  if (vec) {
+    for (int64_t i = 8 * (int64_t)threadIdx.x; i < c.n; i += 8 * 256) {
+      const float4 a = *reinterpret_cast<const float4*>(c.src + i);
+      const float4 b = *reinterpret_cast<const float4*>(c.src + i + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      *reinterpret_cast<uint4*>(dst + i) = pack_f<TO>(v);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < c.n; i += 256) dst[i] = from_f<TO>(c.src[i]);
+  }
+}
+}  // namespace
+
+extern "C" int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, void* dst_base, int32_t dst_dtype,
+                                void* stream) {
+  MC_CHECK(n_chunks >= 0 && (n_chunks == 0 || (chunks && dst_base)), MC_ERR_INVALID, "mc_cast_f32_many: bad chunk table");
+  MC_CHECK(dst_dtype == MC_DTYPE_BF16 || dst_dtype == MC_DTYPE_F16, MC_ERR_DTYPE,
+           "mc_cast_f32_many: dst dtype %d (bf16 / f16 only)", dst_dtype);
+  if (n_chunks == 0) return MC_OK;
+  if (dst_dtype == MC_DTYPE_BF16)
+    hipLaunchKernelGGL(cast_many_kernel<bf16_t>, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, chunks,
+                       reinterpret_cast<bf16_t*>(dst_base));
+  else
+    hipLaunchKernelGGL(cast_many_kernel<f16_t>, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, chunks,
+                       reinterpret_cast<f16_t*>(dst_base));
+  return check_launch("mc_cast_f32_many");
+}

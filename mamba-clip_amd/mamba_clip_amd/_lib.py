@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB", os.path.join(_HERE, "libmamba_cl
 MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3 = 0, 1, 2, 3
 MC_SCAN_CHUNK = 32
 MC_SCAN_MAX_DSTATE = 32
+MC_CAST_CHUNK = 16384
 
 c_i32, c_i64, c_vp, c_fp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p
 
@@ -118,6 +119,7 @@ class AttnBwdParams(ctypes.Structure):
         ("q", c_vp), ("k", c_vp), ("v", c_vp), ("q_bs", c_i64), ("q_ns", c_i64), ("q_hs", c_i64),
         ("o", c_vp), ("dout", c_vp), ("o_bs", c_i64), ("o_ns", c_i64), ("o_hs", c_i64), ("lse", c_fp),
         ("dq", c_vp), ("dk", c_vp), ("dv", c_vp), ("dq_bs", c_i64), ("dq_ns", c_i64), ("dq_hs", c_i64),
+        ("dsum", c_fp),
     ]
 
 
@@ -165,6 +167,7 @@ SYMBOLS = {
                                    ctypes.c_size_t, c_vp]),
     "mc_qkv_grad_pack": (ctypes.c_int, [ctypes.POINTER(QkvPackParams), c_vp]),
     "mc_stream_copy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "mc_cast_f32_many": (ctypes.c_int, [c_i32, c_vp, c_vp, c_i32, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),
 }

@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .ops import (GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d, fc1_gelu,
-                  linear_sk, packed_attention, patch_im2col, qkv_proj, split_rows, wleft_mm)
+                  linear_sk, packed_attention, patch_im2col, qkv_proj, split_rows, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
@@ -368,9 +368,13 @@ class ClipModel(nn.Module):
         return F.normalize(f, dim=-1) if normalize else f
 
     def forward(self, image, text, secondary_text=None):
-        image_features = self.encode_image(image, normalize=True) if image is not None else None
-        text_features = self.encode_text(text, normalize=True) if text is not None else None
-        secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
+        # under CUDA autocast: the towers' Linear weights cast to 16 bits in one launch for this
+        # forward (ops.weight_cast_scope) instead of one cast per weight and use
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
+        with weight_cast_scope(self, dt):
+            image_features = self.encode_image(image, normalize=True) if image is not None else None
+            text_features = self.encode_text(text, normalize=True) if text is not None else None
+            secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
         if self.output_dict:
             out = {"image_features": image_features, "text_features": text_features,
                    "logit_scale": self.logit_scale.exp()}

@@ -583,6 +583,85 @@ def wgrad(G, X):
     return torch.bmm(Gs, Xs, out_dtype=torch.float32).sum(0)
 
 
+# ---------------------------------------------------------------------------- per-forward weight casts (mc_cast_f32_many)
+# Under autocast every projection casts its fp32 weight (and bias) to bf16 on each use: ~230
+# single-tensor cast launches per C2 step.  weight_cast_scope(model, dt) casts all of a model's
+# Linear parameters in ONE launch into a fresh buffer at the start of its forward; the autograd
+# functions below take their 16-bit weights from it (_wcast).  The scope ends with the forward, so
+# a copy is never served for a later forward (parameters may have changed); the backward uses the
+# copies its forward saved, exactly as with per-use casts.
+_WCAST = None   # {id(param): (param, 16-bit copy)} while a scope is active
+_CAST_PLANS = {}
+
+
+def _wcast(t, dt):
+    """t.to(dt), served from the active weight_cast_scope when t is one of its parameters."""
+    if t.dtype == dt:
+        return t
+    if _WCAST is not None:
+        e = _WCAST.get(id(t))
+        if e is not None and e[0] is t and e[1].dtype == dt:
+            return e[1]
+    return t.to(dt)
+
+
+class _CastPlan:
+    """Chunk table (device) and buffer layout for one parameter set."""
+
+    def __init__(self, params, dt, device):
+        offs, off = [], 0
+        rows = []
+        for p in params:
+            offs.append(off)
+            n = p.numel()
+            for s0 in range(0, n, _lib.MC_CAST_CHUNK):
+                rows.append((p.data_ptr() + 4 * s0, off + s0, min(_lib.MC_CAST_CHUNK, n - s0)))
+            off += (n + 7) // 8 * 8                     # 16-B aligned slices
+        self.offs, self.total, self.dt = offs, off, dt
+        self.nchunks = len(rows)
+        self.table = torch.tensor(rows, dtype=torch.int64).to(device)   # mc_cast_chunk = 3 x 8 B
+
+    def run(self, params):
+        buf = torch.empty(self.total, device=self.table.device, dtype=self.dt)
+        _lib.check(_lib.load().mc_cast_f32_many(self.nchunks, self.table.data_ptr(), buf.data_ptr(),
+                                                _lib.dtype_code(self.dt), _lib.stream_handle(buf.device)),
+                   "mc_cast_f32_many")
+        return [buf[o:o + p.numel()].view(p.shape) for o, p in zip(self.offs, params)]
+
+
+class weight_cast_scope:
+    """Context manager: one-launch 16-bit copies of `module`'s Linear weights / biases for one forward
+    (no-op off the GPU, outside autocast, or when nested)."""
+
+    def __init__(self, module, dt):
+        self.module, self.dt, self.active = module, dt, False
+
+    def __enter__(self):
+        global _WCAST
+        if _WCAST is not None or self.dt not in (torch.bfloat16, torch.float16):
+            return self
+        params = [p for m in self.module.modules() if isinstance(m, torch.nn.Linear)
+                  for p in (m.weight, m.bias)
+                  if p is not None and p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()]
+        if not params:
+            return self
+        key = (id(self.module), self.dt, tuple((p.data_ptr(), p.numel()) for p in params))
+        plan = _CAST_PLANS.get(key[:2])
+        if plan is None or plan[0] != key:
+            plan = (key, _CastPlan(params, self.dt, params[0].device))
+            _CAST_PLANS[key[:2]] = plan
+        copies = plan[1].run(params)
+        _WCAST = {id(p): (p, c) for p, c in zip(params, copies)}
+        self.active = True
+        return self
+
+    def __exit__(self, *exc):
+        global _WCAST
+        if self.active:
+            _WCAST = None
+        return False
+
+
 def _compute_dtype(t):
     if t.is_cuda and torch.is_autocast_enabled("cuda"):
         return torch.get_autocast_dtype("cuda")
@@ -595,8 +674,8 @@ class LinearSK(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         dt = _compute_dtype(x)
-        xc, wc = x.to(dt), weight.to(dt)
-        bc = bias.to(dt) if bias is not None else None
+        xc, wc = x.to(dt), _wcast(weight, dt)
+        bc = _wcast(bias, dt) if bias is not None else None
         with torch.autocast("cuda", enabled=False):
             y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
@@ -639,7 +718,7 @@ class WeightLeftMM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, X):
         dt = _compute_dtype(X)
-        wc, Xc = weight.to(dt), X.to(dt)
+        wc, Xc = _wcast(weight, dt), X.to(dt)
         with torch.autocast("cuda", enabled=False):
             y = torch.mm(wc, Xc)
         ctx.save_for_backward(wc, Xc)
@@ -687,7 +766,7 @@ class FC1GeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         dt = _compute_dtype(x)
-        xc, wc, bc = x.to(dt), weight.to(dt), bias.to(dt)
+        xc, wc, bc = x.to(dt), _wcast(weight, dt), _wcast(bias, dt)
         with torch.autocast("cuda", enabled=False):
             h = torch.nn.functional.linear(xc, wc, bc)
             a = torch.nn.functional.gelu(h)
@@ -734,7 +813,7 @@ class QKVProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, heads):
         dt = _compute_dtype(x)
-        xc, wc, bc = x.to(dt), weight.to(dt), bias.to(dt)
+        xc, wc, bc = x.to(dt), _wcast(weight, dt), _wcast(bias, dt)
         Bsz, N, C = xc.shape
         with torch.autocast("cuda", enabled=False):
             y = torch.nn.functional.linear(xc, wc, bc)
@@ -840,7 +919,12 @@ class PackedAttentionFn(torch.autograd.Function):
         p.lse = lse.data_ptr()
         p.dq, p.dk, p.dv = dy.data_ptr(), dy.data_ptr() + C * es, dy.data_ptr() + 2 * C * es
         p.dq_bs, p.dq_ns, p.dq_hs = dy.stride(0), dy.stride(1), D
+        # per-batch column sums of dq | dk | dv, taken in the kernel: the qkv bias gradient rides on dy
+        # (LinearSK picks it up instead of a second pass over the (B*N, 3C) gradient)
+        dsum = torch.empty(Bsz, 3 * C, device=y.device, dtype=torch.float32)
+        p.dsum = dsum.data_ptr()
         _lib.check(lib.mc_attn_bwd(p, _lib.stream_handle(y.device)), "mc_attn_bwd")
+        setattr(dy, COLSUM_ATTR, (dsum.sum(0), dy._version))
         return dy, None
 
 

@@ -623,3 +623,38 @@ def test_mamba_mixer_projected_delta_matches_unfused_and_oracle(d_model, L):
         assert rel(gp_f[n], gp_u[n]) < 3e-2, n
     ref = R.mamba_mixer_ref(m, h)   # fp64 on the GPU with the module's parameters
     assert rel(o_f, ref) < 2e-2
+
+
+def test_weight_cast_scope_bitwise_and_model_identical():
+    """ops.weight_cast_scope (mc_cast_f32_many: every Linear weight / bias of a model cast to bf16
+    in one launch per forward) serves exactly torch's .to(bfloat16) bits, odd sizes included, and
+    a bf16-autocast CLIP forward + backward is bitwise the same with and without it."""
+    import mamba_clip_amd.ops as O
+    from mamba_clip_amd.model import build_clip
+    torch.manual_seed(0)
+    lin = torch.nn.Sequential(torch.nn.Linear(37, 53), torch.nn.Linear(53, 16, bias=False),
+                              torch.nn.Linear(4096, 8192)).to(DEV)   # 33.6M elements: several chunks
+    with O.weight_cast_scope(lin, torch.bfloat16):
+        for p in lin.parameters():
+            got = O._wcast(p, torch.bfloat16)
+            assert got.data_ptr() != p.data_ptr() and torch.equal(got, p.to(torch.bfloat16))
+    assert O._WCAST is None
+    model = build_clip("tiny-mamba-clip").to(DEV)
+    images = torch.randn(4, 3, 32, 32, device=DEV)
+    texts = torch.randint(1, 999, (4, 16), device=DEV)
+    runs = []
+    for use in (True, False):
+        model.zero_grad()
+        real = O.weight_cast_scope.__enter__
+        if not use:
+            O.weight_cast_scope.__enter__ = lambda self: self
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(images, texts)
+            (out["image_features"].float().sum() + out["text_features"].float().square().sum()).backward()
+        finally:
+            O.weight_cast_scope.__enter__ = real
+        runs.append([out["image_features"].detach().clone()] + [p.grad.clone() for p in model.parameters()
+                                                                 if p.grad is not None])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
