@@ -192,8 +192,11 @@ class PatchEmbed(nn.Module):
         Bsz = x.shape[0]
         dt = x.dtype if not torch.is_autocast_enabled("cuda") else torch.get_autocast_dtype("cuda")
         cols = patch_im2col(x.to(dt), self.patch)
-        w = self.proj.weight.reshape(self.proj.weight.shape[0], -1).to(dt)
-        out = F.linear(cols, w, self.proj.bias.to(dt) if self.proj.bias is not None else None)
+        w = self.proj.weight.reshape(self.proj.weight.shape[0], -1)
+        if cols.is_cuda:   # split-K weight gradient (ops.wgrad): 188 -> 85 us at C2
+            out = linear_sk(cols, w, self.proj.bias)
+        else:
+            out = F.linear(cols, w.to(dt), self.proj.bias.to(dt) if self.proj.bias is not None else None)
         return out.reshape(Bsz, -1, w.shape[0])
 
 

@@ -565,7 +565,15 @@ def patch_im2col(img, patch):
 # and summing the fp32 partials (one strided-batched GEMM + one reduction)
 # runs 1.3-1.8x faster and keeps the sum in fp32.
 def _split_factor(M, N, K):
-    s = 4 if N * K >= 2_000_000 else 8
+    """Slabs for the token-dim split, from a sweep of the C2 shapes (tools/wgrad_sweep.py,
+    profiles/r03/wgrad_split_sweep.txt): large outputs 4; small outputs (dt_proj, x_proj) and the
+    ViT's long-M medium outputs (qkv, proj, patch embed) 16; Mamba out_proj (M = 20480) 8."""
+    if N * K >= 2_000_000:
+        s = 4
+    elif N * K < 250_000 or M >= 40_000:
+        s = 16
+    else:
+        s = 8
     while s > 1 and M % s:
         s //= 2
     return s
