@@ -35,6 +35,14 @@ def wg(G, X, s):
     return torch.bmm(Gs, Xs, out_dtype=torch.float32).sum(0)
 
 
+def wg_t(G, X, s):
+    """the transposed product X^T G (K x N) per slab, summed, transposed back"""
+    N, M = G.shape
+    Xs = X.unflatten(0, (s, M // s)).transpose(1, 2)        # (s, K, M/s)
+    Gs = G.t().unflatten(0, (s, M // s))                    # (s, M/s, N)
+    return torch.bmm(Xs, Gs, out_dtype=torch.float32).sum(0).t().contiguous()
+
+
 shapes = [("vit qkv", 50432, 2304, 768), ("vit proj", 50432, 768, 768), ("vit fc1", 50432, 3072, 768),
           ("vit fc2", 50432, 768, 3072), ("patch", 50176, 768, 768),
           ("mamba in_proj", 20480, 3072, 768), ("mamba out_proj", 20480, 768, 1536),
@@ -48,4 +56,7 @@ for name, M, N, K in shapes:
         if M % s == 0:
             us = t(lambda s=s: wg(G, x, s))
             res.append(f"s{s} {us:6.1f} us ({2 * M * N * K / us / 1e6:5.0f} TF/s)")
+            if "--t" in sys.argv:
+                ut = t(lambda s=s: wg_t(G, x, s))
+                res.append(f"T{s} {ut:6.1f}")
     print(f"{name:15s} N{N} K{K} M{M}: " + " | ".join(res), flush=True)
