@@ -34,6 +34,23 @@ __device__ __forceinline__ void st_f32v(float* __restrict__ p, const float (&v)[
     *reinterpret_cast<float4*>(p + e4) = make_float4(v[e4], v[e4 + 1], v[e4 + 2], v[e4 + 3]);
 }
 
+// Sum over the 64 lanes, the same bits in every lane: an xor butterfly on VALU only (DPP inside
+// 16-lane rows, permlane swaps across rows) instead of six ds_bpermute round trips.
+__device__ __forceinline__ float wave_allsum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));   // lane ^ 1
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));   // lane ^ 2
+  {                                                                                                // lane ^ 4
+    const int iv = __float_as_int(v);
+    const int lo = __builtin_amdgcn_update_dpp(iv, iv, 0x104, 0xF, 0x5, false);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(lo, iv, 0x114, 0xF, 0xA, false));
+  }
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));  // lane ^ 8
+  const auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);                                          // lane ^ 16
+  const auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p32[0]) + __uint_as_float(p32[1]);                                       // lane ^ 32
+}
+
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols, const T* __restrict__ x,
                                                               const float* __restrict__ res_in,
@@ -72,8 +89,7 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
         for (int e = 0; e < V; ++e) ss = fmaf(h[i][e], h[i][e], ss);
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    ss = wave_allsum(ss);
     const float rs = rsqrtf(ss / cols + eps);
     if (lane == 0) rstd[row] = rs;
 #pragma unroll
@@ -132,8 +148,7 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dot += __shfl_xor(dot, o);
+    dot = wave_allsum(dot);
     const float c = dot * rs * rs / cols;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -256,8 +271,7 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
         for (int e = 0; e < V; ++e) sum += h[i][e];
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+    sum = wave_allsum(sum);
     const float mu = sum / cols;
     float ss = 0.f;
 #pragma unroll
@@ -267,8 +281,7 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
 #pragma unroll
         for (int e = 0; e < V; ++e) { const float c = h[i][e] - mu; ss = fmaf(c, c, ss); }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    ss = wave_allsum(ss);
     const float rs = rsqrtf(ss / cols + eps);
     if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
 #pragma unroll
@@ -309,21 +322,42 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
     for (int e = 0; e < V; ++e) { dwacc[i][e] = 0.f; dbacc[i][e] = 0.f; if constexpr (kDxSum) dxacc[i][e] = 0.f; }
     if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
   }
+  // one wave per row, the NEXT row's dy / h / dh in flight during this row's math (the kernel is
+  // latency-bound at two waves per SIMD otherwise: two dependent HBM round trips per row)
+  uint4 qd[NV], qh[NV], qr[NV];
+  auto load = [&](int row, uint4 (&a)[NV], uint4 (&b)[NV], uint4 (&c)[NV]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = lane + 64 * i;
+      a[i] = b[i] = c[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        a[i] = ld16(dy + off);
+        b[i] = ld16(hbuf + off);
+        if (dh) c[i] = ld16(dh + off);
+      }
+    }
+  };
+  constexpr bool kPrefetch = NV <= 2;   // wider rows: registers for one row only (no spills)
+  if (kPrefetch && wave < rows) load(wave, qd, qh, qr);
   for (int row = wave; row < rows; row += nwaves) {
     const float mu = mean[row], rs = rstd[row];
+    uint4 nd[NV], nh[NV], nr[NV];
+    if constexpr (kPrefetch) {
+      if (row + nwaves < rows) load(row + nwaves, nd, nh, nr);
+    } else {
+      load(row, qd, qh, qr);
+    }
     float xh[NV][V], g[NV][V];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
-        const int64_t off = (int64_t)row * cols + v * V;
-        const uint4 q = ld16(dy + off);
-        const uint4 hq = ld16(hbuf + off);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          const float d = elem_f<T>(q, e);
-          xh[i][e] = (elem_f<T>(hq, e) - mu) * rs;
+          const float d = elem_f<T>(qd[i], e);
+          xh[i][e] = (elem_f<T>(qh[i], e) - mu) * rs;
           g[i][e] = d * wr[i][e];
           sg += g[i][e];
           sgx = fmaf(g[i][e], xh[i][e], sgx);
@@ -332,11 +366,8 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      sg += __shfl_xor(sg, o);
-      sgx += __shfl_xor(sgx, o);
-    }
+    sg = wave_allsum(sg);
+    sgx = wave_allsum(sgx);
     const float mg = sg / cols, mgx = sgx / cols;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -344,12 +375,10 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
       if (v < nvec) {
         const int64_t off = (int64_t)row * cols + v * V;
         float o[V];
-        uint4 dq = make_uint4(0u, 0u, 0u, 0u);
-        if (dh) dq = ld16(dh + off);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           o[e] = rs * (g[i][e] - mg - xh[i][e] * mgx);
-          if (dh) o[e] += elem_f<T>(dq, e);
+          if (dh) o[e] += elem_f<T>(qr[i], e);
         }
         const uint4 oq = pack_f<T>(o);
         st16(dx + off, oq);
@@ -357,6 +386,14 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
 #pragma unroll
           for (int e = 0; e < V; ++e) dxacc[i][e] += elem_f<T>(oq, e);
         }
+      }
+    }
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        qd[i] = nd[i];
+        qh[i] = nh[i];
+        qr[i] = nr[i];
       }
     }
   }
