@@ -20,6 +20,8 @@
 // g(m) = m ^ ((m & 1) << 2): the row reads of the 32x32x16 operands (ds_read_b128, 16 rows of
 // one chunk per lane group) and the transposed reads (rows r..r+3 x 4 chunks per half-wave) are
 // both conflict-free (64 banks x 4 B).
+#include <algorithm>
+
 #include "mc_common.h"
 #include "../../include/mc_attn.h"
 
@@ -151,6 +153,16 @@ __device__ __forceinline__ void store_rows(TI* base, int64_t ns, int row, int nr
   }
 }
 
+// One global_load_lds_dwordx4: 16 B per lane from gsrc to LDS byte address m0v + 16 * lane (m0v
+// wave-uniform), asm so hipcc does not track it (the caller waits with its own vmcnt); M0 is
+// compiler-reserved: saved and restored in the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0v) : "memory");
+}
+typedef __attribute__((address_space(3))) char lds_char;
+
 struct FwdArgs {
   int B, H, N;
   float scale, c2;   // c2 = scale * log2(e)
@@ -276,17 +288,52 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int Np = NT * 32;
   constexpr int kImg = Np * kRowB;
+  // N <= 224: persistent over heads with the next head's q / dO / O streamed into LDS during phase 2
+  // (the images fit 160 KB with the O staging image); N = 256: one head per workgroup
+  constexpr bool kPersist = NT <= 7;
   char* qimg = smem;
   char* kimg = smem + kImg;
   char* vimg = smem + 2 * kImg;
   char* gimg = smem + 3 * kImg;
-  float* lse2 = reinterpret_cast<float*>(smem + 4 * kImg);   // lse * log2(e); +inf past N (P = 0)
-  float* dlt = lse2 + Np;                                      // rowsum(dO o O)
-  float* csl = dlt + Np;                                       // [dq | dk | dv][wave][64] tile column sums
+  char* oimg = smem + 4 * kImg;                                              // kPersist only
+  float* lse2 = reinterpret_cast<float*>(smem + (kPersist ? 5 : 4) * kImg);   // lse * log2(e); +inf past N (P = 0)
+  float* dlt = lse2 + Np;                                                     // rowsum(dO o O)
+  float* csl = dlt + Np;                                                      // [dq | dk | dv][wave][64] tile column sums
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hh = lane >> 5, l32 = lane & 31, g16 = 16 * ((lane >> 4) & 1);
-  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
-  const int N = a.N;
+  const int N = a.N, total = a.B * a.H;
+  constexpr int kPer = (Np * 8 + 64 * kBwdWaves - 1) / (64 * kBwdWaves);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)smem);
+
+  // q / dO / O rows of head bh -> qimg / gimg / oimg by LDS-DMA (lane-linear 1-KB pieces = 8 rows:
+  // lane L takes slot L % 8 of row L / 8 and loads the chunk that belongs there, c = slot ^ g(row);
+  // rows past N repeat row N - 1, harmless: their P and dS are 0, their outputs are not stored)
+  float lv = 0.f;
+  auto dma_qgo = [&](int bh) __attribute__((always_inline)) {
+    const int b = bh / a.H, h = bh % a.H;
+    const TI* qg = reinterpret_cast<const TI*>(a.q) + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const TI* gg = reinterpret_cast<const TI*>(a.g) + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+    const TI* og = reinterpret_cast<const TI*>(a.o) + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+#pragma unroll
+    for (int k = 0; k < (Np / 8 + kBwdWaves - 1) / kBwdWaves; ++k) {
+      const int j = wave + kBwdWaves * k;
+      if (j < Np / 8) {
+        const uint32_t blk = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(1024 * j));   // wave-uniform M0 base
+        const int r = 8 * j + (lane >> 3), m = (r >> 1) & 7;
+        const int c = (lane & 7) ^ (m ^ ((m & 1) << 2));
+        const int64_t rr = min(r, N - 1);
+        glds16(qg + rr * a.q_ns + 8 * c, blk);
+        glds16(gg + rr * a.o_ns + 8 * c, blk + (uint32_t)(3 * kImg));
+        glds16(og + rr * a.o_ns + 8 * c, blk + (uint32_t)(4 * kImg));
+      }
+    }
+    if (tid < Np) lv = a.lse[(int64_t)bh * N + min(tid, N - 1)];
+  };
+  if constexpr (kPersist) dma_qgo(blockIdx.x);
+
+#pragma unroll 1
+  for (int bh = blockIdx.x; bh < total; bh += gridDim.x) {
+  const int b = bh / a.H, h = bh % a.H;
   const int64_t off = (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
   const int64_t offo = (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
   const TI* qg = reinterpret_cast<const TI*>(a.q) + off;
@@ -295,9 +342,42 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
   const TI* og = reinterpret_cast<const TI*>(a.o) + offo;
   const TI* gg = reinterpret_cast<const TI*>(a.g) + offo;
 
+  if constexpr (kPersist) {
+    // ---- K / V of this head (registers -> images), delta from the streamed dO / O images, lse2
+    const uint32_t rq = (uint32_t)(((int64_t)(N - 1) * a.q_ns + kD) * (int64_t)sizeof(TI));
+    const __amdgpu_buffer_rsrc_t rsk = make_rsrc(kg, rq), rsv = make_rsrc(vg, rq);
+    uint4 kv[kPer], vv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = tid + 64 * kBwdWaves * j, r = i >> 3, c = i & 7;
+      const uint32_t o1 = r < N ? (uint32_t)(r * a.q_ns + 8 * c) * (uint32_t)sizeof(TI) : 0x80000000u;
+      kv[j] = buf_ld16(rsk, o1);
+      vv[j] = buf_ld16(rsv, o1);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's LDS-DMA pieces (and K / V) landed
+    __syncthreads();                      // ... and everyone's
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = tid + 64 * kBwdWaves * j, r = i >> 3, c = i & 7;
+      float part = 0.f;
+      if (i < Np * 8) {
+        const uint4 gq = row_chunk(gimg, r, c), oq = row_chunk(oimg, r, c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part += elem_f<TI>(gq, e) * elem_f<TI>(oq, e);
+      }
+      part += __shfl_xor(part, 1);
+      part += __shfl_xor(part, 2);
+      part += __shfl_xor(part, 4);
+      if (i < Np * 8) {
+        *reinterpret_cast<uint4*>(kimg + img_off(r, c)) = kv[j];
+        *reinterpret_cast<uint4*>(vimg + img_off(r, c)) = vv[j];
+        if (c == 0) dlt[r] = r < N ? part : 0.f;
+      }
+    }
+    if (tid < Np) lse2[tid] = tid < N ? lv * kLog2e : __builtin_huge_valf();
+  } else {
   // ---- prologue: four images, delta and lse2.  Every piece of a thread in flight at once (buffer
   // loads: rows past N read 0); 8 consecutive threads hold one row (delta's partial dots)
-  constexpr int kPer = (Np * 8 + 64 * kBwdWaves - 1) / (64 * kBwdWaves);
   {
     const uint32_t rq = (uint32_t)(((int64_t)(N - 1) * a.q_ns + kD) * (int64_t)sizeof(TI));
     const uint32_t ro = (uint32_t)(((int64_t)(N - 1) * a.o_ns + kD) * (int64_t)sizeof(TI));
@@ -335,6 +415,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
         }
       }
     }
+  }
   }
   __syncthreads();
 
@@ -388,15 +469,23 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
   }
 
   // ---- phase 2: wave = query block; dQ^T += K^T dS^T over the key tiles (forward orientation)
+  const int qt = wave, q = qt * 32 + l32;
+  uint4 qf[4], gf[4];
+  float L = 0.f, Dl = 0.f;
   if (wave < NT) {
-    const int qt = wave, q = qt * 32 + l32;
-    uint4 qf[4], gf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       qf[s] = row_chunk(qimg, q, 2 * s + hh);
       gf[s] = row_chunk(gimg, q, 2 * s + hh);
     }
-    const float L = lse2[q], Dl = dlt[q];
+    L = lse2[q];
+    Dl = dlt[q];
+  }
+  if constexpr (kPersist) {   // q / dO images and the row constants are free: stream the next head's
+    __syncthreads();
+    if (bh + (int)gridDim.x < total) dma_qgo(bh + gridDim.x);
+  }
+  if (wave < NT) {
     f32x16 dq0 = {}, dq1 = {};
 #pragma unroll 1
     for (int kt = 0; kt < NT; ++kt) {
@@ -433,10 +522,24 @@ __global__ __launch_bounds__(64 * kBwdWaves, 1) void attn_bwd_kernel(const BwdAr
       a.dsum[(((int64_t)b * 3 + o) * a.H + h) * kD + d] = acc;
     }
   }
+  __syncthreads();   // images, row constants and column sums are reused by the next head
+  }
 }
 
 size_t fwd_lds(int NT) { return (size_t)2 * NT * 32 * kRowB; }
-size_t bwd_lds(int NT) { return (size_t)4 * NT * 32 * kRowB + (size_t)2 * NT * 32 * 4 + (size_t)3 * kBwdWaves * kD * 4; }
+size_t bwd_lds(int NT) {
+  return (size_t)(NT <= 7 ? 5 : 4) * NT * 32 * kRowB + (size_t)2 * NT * 32 * 4 + (size_t)3 * kBwdWaves * kD * 4;
+}
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
 
 template <typename TI, int NT>
 void launch_fwd_nt(const FwdArgs& a, hipStream_t s) {
@@ -444,7 +547,9 @@ void launch_fwd_nt(const FwdArgs& a, hipStream_t s) {
 }
 template <typename TI, int NT>
 void launch_bwd_nt(const BwdArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((attn_bwd_kernel<TI, NT>), dim3(a.B * a.H), dim3(64 * kBwdWaves), bwd_lds(NT), s, a);
+  // NT <= 7: persistent, one workgroup per CU walks the heads (the LDS of one head fills the CU)
+  const int grid = NT <= 7 ? std::min(a.B * a.H, num_cus()) : a.B * a.H;
+  hipLaunchKernelGGL((attn_bwd_kernel<TI, NT>), dim3(grid), dim3(64 * kBwdWaves), bwd_lds(NT), s, a);
 }
 template <typename TI>
 void launch_fwd(const FwdArgs& a, hipStream_t s) {

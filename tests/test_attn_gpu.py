@@ -123,3 +123,30 @@ def test_tower_attention_fused_matches_sdpa(N):
     assert _nerr(gxf, gxu) < 2e-2
     for n in gpu:
         assert _nerr(gpf[n], gpu[n]) < 2e-2, n
+
+
+@pytest.mark.parametrize("N", [64, 197])
+def test_packed_attention_many_heads_persistent_backward(N):
+    """More (batch, head) pairs than CUs: the persistent backward walks several heads per workgroup and
+    streams the next head's q / dO / O into LDS during phase 2 -- every head must match the fp64
+    reference (reference on the GPU in fp64, same 16-bit inputs)."""
+    from mamba_clip_amd.ops import packed_attention
+    g = torch.Generator().manual_seed(N + 1)
+    B, H, D = 40, 12, 64            # 480 heads > 256 CUs
+    C = H * D
+    qkv = _packed(B, N, H, D, torch.bfloat16, g).requires_grad_(True)
+    o = packed_attention(qkv, H)
+    go = torch.randn(B, N, C, generator=g).to(torch.bfloat16).to(DEV)
+    o.backward(go)
+    ref_in = qkv.detach().double().requires_grad_(True)
+    q, k, v = ref_in.view(B, N, 3, H, D).unbind(2)
+    ro, _ = _ref(q, k, v, D ** -0.5)
+    ro.reshape(B, N, C).backward(go.double())
+    assert _nerr(o, ro.reshape(B, N, C)) < 8e-3
+    got = qkv.grad.view(B, N, 3, H, D).double()
+    want = ref_in.grad.view(B, N, 3, H, D)
+    for bh in range(0, B * H, 37):     # per-head check on a spread of heads (any mix-up shows per head)
+        b, h = divmod(bh, H)
+        for s in range(3):
+            assert _nerr(got[b, :, s, h], want[b, :, s, h], 1e-3 * want[b, :, s, h].norm().item() + 1e-12) < 3e-2, (b, h, s)
+    assert _nerr(got, want) < 2e-2
