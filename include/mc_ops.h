@@ -115,6 +115,12 @@ int mc_qkv_grad_pack(const mc_qkv_pack_params* p, void* stream);
  * HBM streaming rate next to the 8 TB/s spec.  16-B aligned, nbytes % 16 == 0. */
 int mc_stream_copy(const void* src, void* dst, size_t nbytes, void* stream);
 
+/* mc_sum_slabs: dst[i] = sum_{k < s} src[k * slab_stride + i], i < n, fp32, the slabs added in
+ * order k = 0, 1, ... (deterministic).  The slab sum of the towers' split-K weight gradients
+ * (ops.wgrad: s strided-batched GEMM partials over the token dimension); one coalesced pass with
+ * 16-B loads when n, slab_stride and the pointers allow. */
+int mc_sum_slabs(int32_t s, int64_t n, const float* src, int64_t slab_stride, float* dst, void* stream);
+
 /* mc_cast_f32_many: dst_base[c.dst_off + i] = (dtype) c.src[i], i < c.n, for every chunk c, in ONE
  * launch (RNE: the bits of torch's .to(bfloat16 / float16)).  The towers' projection weights are
  * cast once per forward instead of one cast kernel per weight and use (~230 launches per C2 step).

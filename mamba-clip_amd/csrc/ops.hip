@@ -1118,3 +1118,38 @@ extern "C" int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, v
                        reinterpret_cast<f16_t*>(dst_base));
   return check_launch("mc_cast_f32_many");
 }
+
+// ---------------------------------------------------------------------------- split-K slab sums
+namespace {
+template <bool kVec>
+__global__ __launch_bounds__(256) void sum_slabs_kernel(int s, int64_t n, const float* __restrict__ src, int64_t stride,
+                                                        float* __restrict__ dst) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * (kVec ? 4 : 1);
+  if (i0 >= n) return;
+  if constexpr (kVec) {
+    float4 acc = *reinterpret_cast<const float4*>(src + i0);
+    for (int k = 1; k < s; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * stride + i0);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(dst + i0) = acc;
+  } else {
+    float acc = src[i0];
+    for (int k = 1; k < s; ++k) acc += src[(int64_t)k * stride + i0];
+    dst[i0] = acc;
+  }
+}
+}  // namespace
+
+extern "C" int mc_sum_slabs(int32_t s, int64_t n, const float* src, int64_t slab_stride, float* dst, void* stream) {
+  MC_CHECK(s >= 1 && n >= 0 && slab_stride >= n, MC_ERR_SHAPE, "mc_sum_slabs: bad shape (s %d, n %lld, stride %lld)", s,
+           (long long)n, (long long)slab_stride);
+  if (n == 0) return MC_OK;
+  MC_CHECK(src && dst, MC_ERR_INVALID, "mc_sum_slabs: null pointer");
+  const bool vec = n % 4 == 0 && slab_stride % 4 == 0 && aligned16(src) && aligned16(dst);
+  const int64_t items = vec ? n / 4 : n;
+  const dim3 grid((unsigned)((items + 255) / 256));
+  if (vec) hipLaunchKernelGGL(sum_slabs_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, s, n, src, slab_stride, dst);
+  else hipLaunchKernelGGL(sum_slabs_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, s, n, src, slab_stride, dst);
+  return check_launch("mc_sum_slabs");
+}

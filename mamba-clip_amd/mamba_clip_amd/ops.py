@@ -588,7 +588,12 @@ def wgrad(G, X):
         return torch.mm(G, X).float()
     Gs = G.unflatten(1, (s, M // s)).transpose(0, 1)        # (s, N, M/s)
     Xs = X.unflatten(0, (s, M // s))                        # (s, M/s, K)
-    return torch.bmm(Gs, Xs, out_dtype=torch.float32).sum(0)
+    part = torch.bmm(Gs, Xs, out_dtype=torch.float32).contiguous()   # (s, N, K) fp32 slab partials
+    out = torch.empty(N, K, device=part.device, dtype=torch.float32)
+    # one coalesced pass over the slabs in a fixed order (torch's dim-0 sum ran at ~3 TB/s)
+    _lib.check(_lib.load().mc_sum_slabs(s, N * K, part.data_ptr(), part.stride(0), out.data_ptr(),
+                                        _lib.stream_handle(part.device)), "mc_sum_slabs")
+    return out
 
 
 # ---------------------------------------------------------------------------- per-forward weight casts (mc_cast_f32_many)

@@ -658,3 +658,18 @@ def test_weight_cast_scope_bitwise_and_model_identical():
                                                                  if p.grad is not None])
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,N,K", [(50432, 2304, 768), (20480, 80, 1536), (20480, 1536, 48), (16384, 37, 5)])
+def test_wgrad_split_k_slab_sum(M, N, K):
+    """ops.wgrad (split-K strided-batched GEMM + mc_sum_slabs) against one fp32 GEMM of the same
+    bf16 operands: only the summation order differs.  (37, 5): the scalar slab-sum path."""
+    from mamba_clip_amd.ops import _split_factor, wgrad
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    G = torch.randn(N, M, device=DEV, generator=g).bfloat16()
+    X = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    assert _split_factor(M, N, K) > 1
+    got = wgrad(G, X)
+    ref = G.double() @ X.double()
+    assert got.dtype == torch.float32 and got.shape == (N, K)
+    assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5

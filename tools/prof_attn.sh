@@ -3,7 +3,7 @@
 set -u
 out=gpurun_out/pattn; mkdir -p $out
 export TMPDIR=/tmp
-run() { timeout -s KILL 120 rocprofv3 "$@" --output-format csv -- python tools/time_attn.py --iters 5 ; }
+run() { timeout -s KILL 120 rocprofv3 "$@" --output-format csv -- python tools/time_attn_bwd.py --iters 5 ; }
 run --kernel-trace --stats -d $out/trace -o t > $out/trace.log 2>&1 || { echo trace failed; tail $out/trace.log; exit 1; }
 head -12 $out/trace/t_kernel_stats.csv | cut -d, -f1-8
 run --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE -d $out/p1 -o p > $out/p1.log 2>&1 || { echo p1 failed; tail $out/p1.log; exit 1; }
