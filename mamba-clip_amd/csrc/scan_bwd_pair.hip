@@ -77,6 +77,28 @@ __device__ __forceinline__ float row_xor4(float v) {   // banks 0 / 2 take lane 
   return __int_as_float(__builtin_amdgcn_update_dpp(lo, iv, 0x114, 0xF, 0xA, false));
 }
 
+// Halving stages inside a 16-lane row with bank-masked DPP adds (inline asm: hipcc cannot express
+// a write-masked DPP op).  halve_bit3: lanes with bit 3 clear return a + a[lane ^ 8], the others
+// b + b[lane ^ 8]; halve_bit2: bit 2 clear -> a + a[lane + 4], set -> b + b[lane - 4].  The leading
+// s_nop 1 covers the VALU-write -> DPP-read hazard (hipcc pads nothing inside asm).  Same sums,
+// same order as the select form (own + partner).
+__device__ __forceinline__ float halve_bit3(float a, float b) {
+  float r;
+  asm volatile("s_nop 1\n\t"
+               "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+               "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+               : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float halve_bit2(float a, float b) {
+  float r;
+  asm volatile("s_nop 1\n\t"
+               "v_add_f32_dpp %0, %1, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+               "v_add_f32_dpp %0, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa"
+               : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Sum of 16 per-lane values (8 packed pairs, value k = 2t + s in v[t].{x|y}) over the 32 lanes of
 // the same lane bit 0 (the wave's 32 channels).  Lane l ends with value k = l >> 2 (lanes l and l ^ 2
 // hold the same sum).  Halving stages over lane bits 5, 4 (permlane swaps, packed adds), 3, 2 (DPP),
@@ -95,14 +117,10 @@ __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
     const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[t].y), __float_as_uint(v[t + 2].y), false, false);
     v[t] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
-  const bool b3 = lane & 8, b2 = lane & 4;
-  {   // bit 3: t = 0 <-> 1
-    const f32x2 keep = b3 ? v[1] : v[0], send = b3 ? v[0] : v[1];
-    v[0] = keep + f32x2{row_xor8(send.x), row_xor8(send.y)};
-  }
-  // bit 2: s = 0 <-> 1
-  const float keep = b2 ? v[0].y : v[0].x, send = b2 ? v[0].x : v[0].y;
-  const float r = keep + row_xor4(send);
+  // bit 3: t = 0 <-> 1 and bit 2: s = 0 <-> 1 as bank-masked DPP adds (each half of a 16-lane row
+  // writes its own sum), instead of keep / send selects around a DPP move
+  const float x = halve_bit3(v[0].x, v[1].x), y = halve_bit3(v[0].y, v[1].y);
+  const float r = halve_bit2(x, y);
   return r + qperm<kQpXor2>(r);   // bit 1
 }
 
