@@ -99,6 +99,22 @@ __device__ __forceinline__ float halve_bit2(float a, float b) {
   return r;
 }
 
+// Finishing of one position's state sums: lanes of half h keep pair (h ? b : a) and add the partner
+// lane's (lane ^ 1) other pair, each pair summed over its two states first.  The two pair sums and
+// the DPP add are asm so that the compiler neither SLP-packs the sums (it did, into more
+// instructions) nor keeps the DPP move apart from the add: 2 adds, 2 selects, 1 DPP add instead
+// of 4 selects, 2 adds, a DPP move and an add.  Same sums, same order as before.
+__device__ __forceinline__ float pair_finish(f32x2 a, f32x2 b, int h) {
+  float sa, sb, r;
+  asm("v_add_f32_e32 %0, %1, %2" : "=v"(sa) : "v"(a.x), "v"(a.y));
+  asm("v_add_f32_e32 %0, %1, %2" : "=v"(sb) : "v"(b.x), "v"(b.y));
+  const float keep = h ? sb : sa, send = h ? sa : sb;
+  asm("s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r) : "v"(send), "v"(keep));
+  return r;
+}
+
 // Sum of 16 per-lane values (8 packed pairs, value k = 2t + s in v[t].{x|y}) over the 32 lanes of
 // the same lane bit 0 (the wave's 32 channels).  Lane l ends with value k = l >> 2 (lanes l and l ^ 2
 // hold the same sum).  Halving stages over lane bits 5, 4 (permlane swaps, packed adds), 3, 2 (DPP),
@@ -478,17 +494,12 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
       float fS[4], fQ[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const f32x2 so = h ? S2[4 + e] : S2[e], sp = h ? S2[e] : S2[4 + e];
-        const f32x2 qo = h ? Q2[4 + e] : Q2[e], qp = h ? Q2[e] : Q2[4 + e];
-        fS[e] = (so.x + so.y) + qperm<kQpXor1>(sp.x + sp.y);
-        fQ[e] = ((qo.x + qo.y) + qperm<kQpXor1>(qp.x + qp.y)) * kLn2;   // A2 carries log2(e)
+        fS[e] = pair_finish(S2[e], S2[4 + e], h);
+        fQ[e] = pair_finish(Q2[e], Q2[4 + e], h) * kLn2;   // A2 carries log2(e)
       }
       float fY[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f32x2 yo = h ? Y2[4 + e] : Y2[e], yp = h ? Y2[e] : Y2[4 + e];
-        fY[e] = (yo.x + yo.y) + qperm<kQpXor1>(yp.x + yp.y);
-      }
+      for (int e = 0; e < 4; ++e) fY[e] = pair_finish(Y2[e], Y2[4 + e], h);
       float o_du[4], o_dd[4], o_dz[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
