@@ -27,8 +27,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import (GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d, fc1_gelu,
-                  linear_sk, packed_attention, patch_im2col, qkv_proj, split_rows, weight_cast_scope, wleft_mm)
+from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
+                  fc1_gelu, linear_sk, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
+                  weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
@@ -41,10 +42,10 @@ def _dt_bias_init(d_inner, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
     return dt + torch.log(-torch.expm1(-dt))
 
 
-def mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab):
+def mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None):
     """The mixer's scan call (selective_scan_fn semantics, softplus on) with dz written into
-    the in_proj gradient slab."""
-    return SelectiveScanFn.apply(x, delta, A, Bm, Cm, D, z, delta_bias, True, False, dz_slab)
+    the in_proj gradient slab and du handed to x_proj's backward (ops.GradHandoff)."""
+    return SelectiveScanFn.apply(x, delta, A, Bm, Cm, D, z, delta_bias, True, False, dz_slab, du_handoff)
 
 
 class MambaMixer(nn.Module):
@@ -81,8 +82,9 @@ class MambaMixer(nn.Module):
         # kernels are VALU-bound, so forming delta on their MFMAs costs more than the delta stream it
         # saves (C2 step 88.4 vs 86.5 ms on one box, profiles/r03/c2_ab_fuse_dt_proj.txt)
         self.fuse_dt_proj = False
+        self.du_handoff = True   # scan du -> x_proj's dX epilogue (ops.GradHandoff)
 
-    def forward(self, hidden):  # (B, L, d_model) contiguous
+    def forward(self, hidden, A=None):  # (B, L, d_model) contiguous; A: -exp(A_log) when the tower formed it
         Bsz, L, dm = hidden.shape
         dt_in = hidden.dtype
         di, R, N = self.d_inner, self.dt_rank, self.d_state
@@ -97,7 +99,8 @@ class MambaMixer(nn.Module):
         z = z.view(di, Bsz, L).transpose(0, 1)
         x = causal_conv1d(x, self.conv1d.weight, self.conv1d.bias, silu=True, dx_slab=slab)
         x_cm = x.transpose(0, 1).reshape(di, Bsz * L)                          # view
-        A = -torch.exp(self.A_log.float())
+        if A is None:
+            A = -torch.exp(self.A_log.float())
         dz = (slab, di) if slab is not None else None
         if self.fuse_dt_proj and projected_scan_ok(x, R, N):
             # dt_proj inside the scan (ProjectedScanFn): x_proj's dt rows come out token-major,
@@ -109,12 +112,15 @@ class MambaMixer(nn.Module):
             y = ProjectedScanFn.apply(x, dt_raw, self.dt_proj.weight, A, Bm, Cm, self.D.float(), z,
                                       self.dt_proj.bias.float(), True, dz)
         else:
-            x_dbl = wleft_mm(self.x_proj.weight, x_cm)                         # (R+2N, B*L)
+            # x's gradient: the scan's du is handed to x_proj's backward, which adds its dX in the
+            # GEMM epilogue (ops.GradHandoff) instead of autograd summing the two producers
+            hand = GradHandoff() if (self.du_handoff and x.is_cuda and x.requires_grad) else None
+            x_dbl = wleft_mm(self.x_proj.weight, x_cm, hand)                   # (R+2N, B*L)
             dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
             delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
             Bm = Bm.view(N, Bsz, L).transpose(0, 1)                           # (B, N, L)
             Cm = Cm.view(N, Bsz, L).transpose(0, 1)
-            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz)
+            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz, hand)
         y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
         out = linear_sk(y2.t(), self.out_proj.weight)                          # (B*L, d_model)
         return out.view(Bsz, L, dm)
@@ -129,9 +135,9 @@ class MambaLayer(nn.Module):
         self.norm_weight = nn.Parameter(torch.ones(d_model))
         self.eps = eps
 
-    def forward(self, hidden, residual):
+    def forward(self, hidden, residual, A=None):
         normed, residual = add_rmsnorm(hidden, residual, self.norm_weight, self.eps)
-        return self.mixer(normed), residual
+        return self.mixer(normed, A), residual
 
 
 class MambaTextEncoder(nn.Module):
@@ -169,8 +175,11 @@ class MambaTextEncoder(nn.Module):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
         hidden = self.embedding(tokens).to(dt)
         residual = None
-        for layer in self.layers:
-            hidden, residual = layer(hidden, residual)
+        # every mixer's A = -exp(A_log) in one launch (ops.NegExpManyFn)
+        As = (neg_exp_many([l.mixer.A_log for l in self.layers]) if hidden.is_cuda
+              else [None] * len(self.layers))
+        for layer, A in zip(self.layers, As):
+            hidden, residual = layer(hidden, residual, A)
         normed, _ = add_rmsnorm(hidden, residual, self.norm_f)
         pooled = normed[:, T - 1]                                   # EOT position
         return self.proj(pooled)

@@ -596,6 +596,65 @@ def wgrad(G, X):
     return out
 
 
+def sum_rows(t):
+    """(R, n) fp32 contiguous -> (n,) column sums in a fixed order: two mc_sum_slabs passes (R -> R/16
+    -> 1) when R is a multiple of 16, so each pass has enough workgroups (one pass over R = 256 rows
+    of 2304 -- the attention backward's per-batch sums -- would run 3 workgroups)."""
+    R, n = t.shape
+    lib, st = _lib.load(), _lib.stream_handle(t.device)
+    if R >= 64 and R % 16 == 0:
+        mid = torch.empty(R // 16, n, device=t.device, dtype=torch.float32)
+        _lib.check(lib.mc_sum_slabs(16, (R // 16) * n, t.data_ptr(), (R // 16) * n, mid.data_ptr(), st), "mc_sum_slabs")
+        t, R = mid, R // 16
+    out = torch.empty(n, device=t.device, dtype=torch.float32)
+    _lib.check(lib.mc_sum_slabs(R, n, t.data_ptr(), n, out.data_ptr(), st), "mc_sum_slabs")
+    return out
+
+
+class NegExpManyFn(torch.autograd.Function):
+    """A_i = -exp(A_log_i) for every mixer of a tower in one multi-tensor launch (plus one in-place
+    negation); backward dA_log_i = dA_i * A_i in one launch.  Per mixer this was 4 single-tensor
+    launches (exp, neg; neg, mul) -- reference mixer: A = -torch.exp(self.A_log.float())
+    (model.py:519-528).  Bitwise the same values: negation is exact."""
+
+    @staticmethod
+    def forward(ctx, *logs):
+        outs = torch._foreach_exp([t.float() for t in logs])
+        torch._foreach_neg_(outs)
+        ctx.save_for_backward(*outs)
+        ctx.set_materialize_grads(False)   # an A without a gradient gets none (not a zero pass)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        outs = ctx.saved_tensors
+        idx = [i for i, g in enumerate(gs) if g is not None]
+        res = [None] * len(gs)
+        if idx:
+            for i, v in zip(idx, torch._foreach_mul([gs[i].float() for i in idx], [outs[i] for i in idx])):
+                res[i] = v
+        return tuple(res)
+
+
+def neg_exp_many(logs):
+    return list(NegExpManyFn.apply(*logs))
+
+
+class GradHandoff:
+    """The Mamba mixer's x (conv output) feeds both x_proj and the scan, so its gradient is the sum of
+    x_proj's dX and the scan's du.  The scan backward (which always runs first: x_proj's output
+    gradient needs its ddelta / dB / dC) parks du here and returns no gradient for u; x_proj's
+    backward then accumulates dX onto du in its GEMM epilogue (addmm_, beta = 1), so the separate
+    bf16 add of the two producers -- and its extra pass over the (d_inner, B*L) gradient -- goes."""
+
+    def __init__(self):
+        self.du = None
+
+    def take(self):
+        du, self.du = self.du, None
+        return du
+
+
 # ---------------------------------------------------------------------------- per-forward weight casts (mc_cast_f32_many)
 # Under autocast every projection casts its fp32 weight (and bias) to bf16 on each use: ~230
 # single-tensor cast launches per C2 step.  weight_cast_scope(model, dt) casts all of a model's
@@ -729,12 +788,13 @@ class WeightLeftMM(torch.autograd.Function):
     """y = w @ X for a weight w (N, K) and activations X (K, M) (channel-major GEMMs of the Mamba mixer)."""
 
     @staticmethod
-    def forward(ctx, weight, X):
+    def forward(ctx, weight, X, handoff=None):
         dt = _compute_dtype(X)
         wc, Xc = _wcast(weight, dt), X.to(dt)
         with torch.autocast("cuda", enabled=False):
             y = torch.mm(wc, Xc)
         ctx.save_for_backward(wc, Xc)
+        ctx.handoff = handoff
         return y
 
     @staticmethod
@@ -744,16 +804,26 @@ class WeightLeftMM(torch.autograd.Function):
         dw = dX = None
         if ctx.needs_input_grad[0]:
             dw = wgrad(g, Xc.t())
+        acc = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[1]:
-            if Xc.stride(0) == 1 and Xc.stride(1) != 1:
+            if acc is not None and Xc.stride(1) == 1 and Xc.is_contiguous():
+                # the other consumer's gradient (GradHandoff), in X's layout: dX += w^T g in the epilogue
+                dX = acc.transpose(0, 1).reshape(Xc.shape)
+                if dX.data_ptr() != acc.data_ptr() or not dX.is_contiguous():
+                    raise RuntimeError("wleft_mm backward: handed-off gradient is not in X's layout")
+                dX.addmm_(wc.t(), g)
+                acc = None
+            elif Xc.stride(0) == 1 and Xc.stride(1) != 1:
                 dX = torch.mm(g.t(), wc).t()      # X is a transposed view: keep its layout (no copy downstream)
             else:
                 dX = torch.mm(wc.t(), g)
-        return dw, dX
+            if acc is not None:
+                dX = dX + acc.transpose(0, 1).reshape(Xc.shape)
+        return dw, dX, None
 
 
-def wleft_mm(weight, X):
-    return WeightLeftMM.apply(weight, X)
+def wleft_mm(weight, X, handoff=None):
+    return WeightLeftMM.apply(weight, X, handoff)
 
 
 # ---------------------------------------------------------------------------- fused bias-gradient passes (mc_ops.h)
@@ -937,7 +1007,7 @@ class PackedAttentionFn(torch.autograd.Function):
         dsum = torch.empty(Bsz, 3 * C, device=y.device, dtype=torch.float32)
         p.dsum = dsum.data_ptr()
         _lib.check(lib.mc_attn_bwd(p, _lib.stream_handle(y.device)), "mc_attn_bwd")
-        setattr(dy, COLSUM_ATTR, (dsum.sum(0), dy._version))
+        setattr(dy, COLSUM_ATTR, (sum_rows(dsum), dy._version))
         return dy, None
 
 

@@ -179,7 +179,7 @@ class SelectiveScanFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
-                return_last_state=False, dz_slab=None):
+                return_last_state=False, dz_slab=None, du_handoff=None):
         u, delta, z = _last_dim_contig(u), _last_dim_contig(delta), _last_dim_contig(z)
         squeeze_B, squeeze_C = B.dim() == 3, C.dim() == 3
         B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
@@ -198,6 +198,7 @@ class SelectiveScanFn(torch.autograd.Function):
                       delta_bias.dtype if delta_bias is not None else None)
         ctx.has = (D is not None, z is not None, delta_bias is not None)
         ctx.dz_slab = dz_slab   # (GradSlab, first row): dz written into that slab (ops.GradSlab)
+        ctx.du_handoff = du_handoff   # ops.GradHandoff: du parked for x_proj's backward (no u gradient here)
         return (out, last) if return_last_state else out
 
     @staticmethod
@@ -214,11 +215,13 @@ class SelectiveScanFn(torch.autograd.Function):
         if ctx.squeeze[1]:
             dC = dC.squeeze(1)
         a_dt, d_dt, b_dt = ctx.dtypes
+        if ctx.du_handoff is not None:
+            ctx.du_handoff.du, du = du, None
         return (du, ddelta, dA.to(a_dt), dB, dC,
                 dD.to(d_dt) if dD is not None else None,
                 dz,
                 dbias.to(b_dt) if dbias is not None else None,
-                None, None, None)
+                None, None, None, None)
 
 
 class ProjectedScanFn(torch.autograd.Function):

@@ -62,7 +62,7 @@ def grouped_scan_ref(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=
     return torch.stack([fl(out[:, g], g) for g in range(G)], 1).reshape(Bsz, dim, L)
 
 
-def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab):
+def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None):
     return selective_scan_ref(x, delta, A, Bm, Cm, D, z=z, delta_bias=delta_bias, delta_softplus=True)
 
 

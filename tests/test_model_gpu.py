@@ -335,6 +335,65 @@ def test_mamba_mixer_xz_gradient_slab_no_concat():
     torch.testing.assert_close(h.grad, gh_slab, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mamba_mixer_du_handoff(dt):
+    """The scan hands du to x_proj's backward (ops.GradHandoff), which adds its dX in the GEMM
+    epilogue: the same gradients as autograd summing the two producers (one rounding instead of two
+    in bf16), and the handoff is consumed."""
+    import mamba_clip_amd.model as M
+    from mamba_clip_amd import ops
+    torch.manual_seed(2)
+    m = M.MambaMixer(128, d_state=16).to(DEV)
+    h = torch.randn(4, 64, 128, device=DEV)
+    gy = torch.randn(4, 64, 128, device=DEV)
+    made = []
+    real = M.GradHandoff
+
+    def spy():
+        made.append(real())
+        return made[-1]
+
+    runs = []
+    for hand in (spy, lambda: None):
+        M.GradHandoff = hand
+        try:
+            m.zero_grad()
+            hh = h.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dt == torch.bfloat16):
+                y = m(hh)
+            (y.float() * gy).sum().backward()
+        finally:
+            M.GradHandoff = real
+        runs.append((hh.grad.clone(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert len(made) == 1 and made[0].du is None          # handed over and taken
+    (gh, gp), (gh0, gp0) = runs
+    tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(gh, gh0, **tol)
+    for n in gp0:
+        torch.testing.assert_close(gp[n], gp0[n], **tol, msg=n)
+    assert isinstance(ops.GradHandoff(), ops.GradHandoff)
+
+
+def test_text_tower_neg_exp_many_bitwise():
+    """The tower forms every mixer's A = -exp(A_log) in one launch (ops.NegExpManyFn): values and
+    A_log gradients bitwise equal to the per-mixer expression."""
+    from mamba_clip_amd.ops import neg_exp_many
+    torch.manual_seed(3)
+    logs = [torch.randn(96, 16, device=DEV, requires_grad=True) for _ in range(5)]
+    gs = [torch.randn(96, 16, device=DEV) for _ in range(5)]
+    As = neg_exp_many(logs)
+    torch.autograd.backward([a for a in As if True][:4], gs[:4])   # one output without a gradient
+    for i, (l, a) in enumerate(zip(logs, As)):
+        ref_l = l.detach().clone().requires_grad_(True)
+        ref = -torch.exp(ref_l.float())
+        assert torch.equal(a, ref.detach())
+        if i < 4:
+            ref.backward(gs[i])
+            assert torch.equal(l.grad, ref_l.grad)
+        else:
+            assert l.grad is None
+
+
 @pytest.mark.parametrize("fname", ["ss2d_d32_h6w5.safetensors", "ss2d_d16_h4w4.safetensors"])
 def test_ss2d_matches_reference_golden(fname):
     from mamba_clip_amd.model import SS2D
@@ -361,13 +420,16 @@ def test_ss_conv_ssm_matches_reference_golden():
 def test_tiny_clip_train_step():
     from mamba_clip_amd.model import init_model
     from mamba_clip_amd.loss import ClipLoss
+    # seeded, lr 3e-4 over 5 steps: at lr 1e-3 / 3 steps the loss rose on some seeds with or
+    # without any given fusion (tools/dbg_tiny.py), i.e. the old form was a flaky check
+    torch.manual_seed(0)
     model, _, _, _ = init_model("tiny-mamba-clip")
     model = model.to(DEV)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    opt = torch.optim.AdamW(model.parameters(), lr=3e-4)
     img = torch.randn(8, 3, 32, 32, device=DEV)
     tok = torch.randint(1, 1000, (8, 16), device=DEV)
     losses = []
-    for _ in range(3):
+    for _ in range(5):
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = model(img, tok)
             loss = ClipLoss()(**out)["contrastive_loss"]
