@@ -470,20 +470,26 @@ __device__ __forceinline__ void load_window(const T* __restrict__ xr, int t0, in
 }
 
 // KC: the tap count as a compile-time constant (4: Mamba's d_conv) or 0 = runtime K <= kMaxK.
+// Items walk the rows in memory order: with the mixer's channel-major views (x_bs = L < x_ds) the
+// batch index varies fastest, so a wave's 64 16-B vectors are one contiguous 1 KiB span (ordering
+// by channel first touched 160-B rows 40 KiB apart, each straddling two 128-B lines).  32-bit
+// index math (the launcher checks the item count).
 template <typename T, int VEC, int KC>
 __global__ __launch_bounds__(256) void conv1d_fwd_kernel(int batch, int dim, int L, int K_, const T* __restrict__ x,
                                                          int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int silu,
-                                                         T* __restrict__ y, int64_t y_bs, int64_t y_ds) {
+                                                         T* __restrict__ y, int64_t y_bs, int64_t y_ds, int bfast) {
   constexpr int KM = KC ? KC : kMaxK;
   const int K = KC ? KC : K_;
   constexpr int NP = (KM - 1 + VEC - 1) / VEC;   // previous vectors covering the K-1 halo
-  const int nchunk = (L + VEC - 1) / VEC;
-  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= (int64_t)batch * dim * nchunk) return;
-  const int64_t row = item / nchunk;
+  const unsigned nchunk = (unsigned)(L + VEC - 1) / VEC;
+  const unsigned item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= (unsigned)batch * (unsigned)dim * nchunk) return;
+  const unsigned row = item / nchunk;
   const int t0 = (int)(item - row * nchunk) * VEC;
-  const int b = (int)(row / dim), d = (int)(row - (int64_t)b * dim);
+  int b, d;
+  if (bfast) { d = (int)(row / (unsigned)batch); b = (int)(row - (unsigned)d * batch); }
+  else { b = (int)(row / (unsigned)dim); d = (int)(row - (unsigned)b * dim); }
   const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
   float win[(NP + 1) * VEC];
   load_window<T, VEC, NP, 0>(xr, t0, L, win);
@@ -601,6 +607,93 @@ __global__ __launch_bounds__(256) void conv1d_bwd_kernel(int batch, int dim, int
   }
 }
 
+// Backward for vector rows and Mamba's K = 4 (K - 1 <= VEC): lane l takes item base + l, so lane
+// l + 1 holds the next VEC positions of the same row.  Each lane forms g = dy * act'(pre) for its own
+// VEC positions only and takes the K - 1 halo values g[t0 + VEC ..] from lane l + 1 (one shuffle
+// each); the wave advances by 63 items, lane 63 forming g only as lane 62's halo.  Against the
+// generic kernel: 8 instead of 11 sigmoids per item, and neither the x vector after the item nor
+// the next dy vector is loaded.  Same sums, same order (g values are bit-identical either way).
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void conv1d_bwd_halo_kernel(int batch, int dim, int L, const T* __restrict__ x,
+                                                              int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, int silu,
+                                                              const T* __restrict__ dy, int64_t dy_bs, int64_t dy_ds,
+                                                              T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
+                                                              int items_per_slice, float* __restrict__ part) {
+  constexpr int K = 4;
+  static_assert(K - 1 <= VEC, "halo from one neighbour");
+  const int lane = threadIdx.x & 63;
+  const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= dim) return;   // whole wave: the shuffles below see all 64 lanes
+  const int slice = blockIdx.y;
+  const int nchunk = (L + VEC - 1) / VEC;
+  const int total = batch * nchunk;
+  const int i_begin = slice * items_per_slice;
+  const int i_end = min(total, i_begin + items_per_slice);
+  float wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[d * K + k];
+  const float bv = bias ? bias[d] : 0.f;
+  float dwk[K] = {0.f, 0.f, 0.f, 0.f}, db = 0.f;
+  for (int base = i_begin; base < i_end; base += 63) {
+    const int item = base + lane;
+    const bool live = item < total;                      // forms g (lane 63: lane 62's halo)
+    const bool own = lane < 63 && item < i_end;          // writes dx, accumulates dw / db
+    const int it = live ? item : total - 1;
+    const int b = it / nchunk;
+    const int t0 = (it - b * nchunk) * VEC;
+    const T* xr = x + (int64_t)b * x_bs + (int64_t)d * x_ds;
+    float win[2 * VEC];
+    load_window<T, VEC, 1, 0>(xr, t0, L, win);
+    float gy[VEC];
+    load_vec<T, VEC>(dy + (int64_t)b * dy_bs + (int64_t)d * dy_ds + t0, gy);
+    float g[VEC + K - 1];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float pre = bv;
+#pragma unroll
+      for (int k = 0; k < K; ++k) pre = fmaf(wk[k], win[VEC + j - (K - 1) + k], pre);
+      float gj = gy[j];
+      if (silu) {
+        const float s = sigmoid_f(pre);
+        gj *= s * (1.f + pre * (1.f - s));
+      }
+      g[j] = live ? gj : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) {
+      const float h = __shfl_down(g[j], 1);
+      g[VEC + j] = (t0 + VEC + j < L) ? h : 0.f;         // past the row's end: zero (as the generic kernel)
+    }
+    if (own) {
+      float out[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fmaf(wk[k], g[i + (K - 1) - k], acc);
+        out[i] = acc;
+        db += g[i];
+#pragma unroll
+        for (int k = 0; k < K; ++k) dwk[k] = fmaf(g[i], win[VEC + i - (K - 1) + k], dwk[k]);
+      }
+      store_vec<T, VEC>(dx + (int64_t)b * dx_bs + (int64_t)d * dx_ds + t0, out);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) dwk[k] += __shfl_xor(dwk[k], o);
+    db += __shfl_xor(db, o);
+  }
+  if (lane == 0) {
+    float* pr = part + ((int64_t)slice * dim + d) * (kMaxK + 1);
+#pragma unroll
+    for (int k = 0; k < K; ++k) pr[k] = dwk[k];
+    pr[kMaxK] = db;
+  }
+}
+
 // dw[d, k] = sum_s part[s, d, k]; dbias[d] = sum_s part[s, d, kMaxK]   (fixed order)
 __global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restrict__ part, int nslice, int dim, int K,
                                                             float* __restrict__ dw, float* __restrict__ dbias) {
@@ -615,12 +708,15 @@ __global__ __launch_bounds__(256) void conv1d_reduce_kernel(const float* __restr
 }
 
 // batch x chunk items per backward wave: ~4 items per lane
-static inline int conv1d_items_per_slice(int batch, int L, int vec) {
+// (step: items a wave advances per iteration -- 63 for the halo kernel; slices are whole iterations
+// there, so no iteration runs a handful of items)
+static inline int conv1d_items_per_slice(int batch, int L, int vec, int step = 64) {
   const int nchunk = (L + vec - 1) / vec;
   const int total = batch * nchunk;
-  const int target = 64 * 4;            // 4 items per lane: enough waves to hide the load latency
+  const int target = step * 4;          // 4 items per lane: enough waves to hide the load latency
   const int nslice = std::max(1, (total + target - 1) / target);
-  return (total + nslice - 1) / nslice;
+  const int per = (total + nslice - 1) / nslice;
+  return step == 64 ? per : (per + step - 1) / step * step;
 }
 
 // ------------------------------------------------------------------ patch im2col
@@ -912,14 +1008,17 @@ extern "C" int mc_causal_conv1d_fwd(int32_t batch, int32_t dim, int32_t seqlen, 
   const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
   const int vec = seqlen % V == 0 && conv1d_vec_ok(x, x_bs, x_ds, V) && conv1d_vec_ok(y, y_bs, y_ds, V) ? V : 1;
   const int64_t items = (int64_t)batch * dim * ((seqlen + vec - 1) / vec);
+  MC_CHECK(items < (int64_t(1) << 31), MC_ERR_SHAPE, "mc_causal_conv1d_fwd: %lld vector items exceed 2^31",
+           (long long)items);
   const dim3 grid((unsigned)((items + 255) / 256));
+  const int bfast = x_bs < x_ds;   // rows adjacent in memory along the batch (channel-major views)
   MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
     if (K == 4)
       hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC, 4>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen,
-                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
+                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds, bfast);
     else
       hipLaunchKernelGGL((conv1d_fwd_kernel<T, VEC, 0>), grid, dim3(256), 0, (hipStream_t)stream, batch, dim, seqlen,
-                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds);
+                         K, (const T*)x, x_bs, x_ds, w, bias, silu, (T*)y, y_bs, y_ds, bfast);
   }));
   return check_launch("mc_causal_conv1d_fwd");
 }
@@ -952,12 +1051,21 @@ extern "C" int mc_causal_conv1d_bwd(int32_t batch, int32_t dim, int32_t seqlen, 
   const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
   const int vec = seqlen % V == 0 && conv1d_vec_ok(x, x_bs, x_ds, V) && conv1d_vec_ok(dy, dy_bs, dy_ds, V) &&
                           conv1d_vec_ok(dx, dx_bs, dx_ds, V) ? V : 1;
-  const int per = conv1d_items_per_slice(batch, seqlen, vec);
+  const int per = conv1d_items_per_slice(batch, seqlen, vec, (vec > 1 && K == 4) ? 63 : 64);
   const int total = batch * ((seqlen + vec - 1) / vec);
   const int nslice = (total + per - 1) / per;
   const dim3 grid((unsigned)((dim + 3) / 4), (unsigned)nslice);
   MC_DISPATCH_T(dtype, MC_DISPATCH_VEC(vec, if constexpr (VEC == 1 || VEC == ElemTraits<T>::kVec) {
-    if (K == 4)   // Mamba's d_conv: taps unrolled at compile time
+    bool done = false;
+    if constexpr (VEC > 1) {
+      if (K == 4) {   // Mamba's d_conv on vector rows: halo g from the neighbouring lane
+        hipLaunchKernelGGL((conv1d_bwd_halo_kernel<T, VEC>), grid, dim3(256), 0, s, batch, dim, seqlen, (const T*)x,
+                           x_bs, x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
+        done = true;
+      }
+    }
+    if (done) {
+    } else if (K == 4)   // taps unrolled at compile time
       hipLaunchKernelGGL((conv1d_bwd_kernel<T, VEC, 4>), grid, dim3(256), 0, s, batch, dim, seqlen, K, (const T*)x,
                          x_bs, x_ds, w, bias, silu, (const T*)dy, dy_bs, dy_ds, (T*)dx, dx_bs, dx_ds, per, part);
     else

@@ -371,6 +371,24 @@ class ClipModel(nn.Module):
         self.context_length = getattr(self.text, "context_length", None)
         self.vocab_size = getattr(self.text, "vocab_size", None)
 
+    # image and text towers on two HIP streams (ClipModel.forward).  Off under a multi-process group:
+    # DDP launches a gradient bucket's all-reduce behind one stream, and a bucket could then hold
+    # gradients still being written on the other.
+    concurrent_towers = True
+    _side_streams = {}
+
+    def _side_stream(self, image, text):
+        if not (self.concurrent_towers and image is not None and text is not None and image.is_cuda
+                and torch.is_grad_enabled()):
+            return None
+        if torch.distributed.is_available() and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            return None
+        dev = image.device
+        if dev not in ClipModel._side_streams:
+            ClipModel._side_streams[dev] = torch.cuda.Stream(device=dev)
+        return ClipModel._side_streams[dev]
+
     def encode_image(self, image, normalize: bool = False):
         f = self.visual(image)
         return F.normalize(f, dim=-1) if normalize else f
@@ -383,9 +401,24 @@ class ClipModel(nn.Module):
         # under CUDA autocast: the towers' Linear weights cast to 16 bits in one launch for this
         # forward (ops.weight_cast_scope) instead of one cast per weight and use
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
-        with weight_cast_scope(self, dt):
-            image_features = self.encode_image(image, normalize=True) if image is not None else None
-            text_features = self.encode_text(text, normalize=True) if text is not None else None
+        with weight_cast_scope(self, dt) as casts:
+            side = self._side_stream(image, text)
+            if side is None:
+                image_features = self.encode_image(image, normalize=True) if image is not None else None
+                text_features = self.encode_text(text, normalize=True) if text is not None else None
+            else:
+                # the towers are independent until the loss: the text tower runs on a second HIP stream
+                # beside the image tower (its backward follows it there: autograd runs each backward op
+                # on its forward op's stream and joins the streams at the end of backward)
+                main = torch.cuda.current_stream()
+                side.wait_stream(main)                       # the one-launch weight casts, the inputs
+                text.record_stream(side)
+                casts.record_stream(side)
+                with torch.cuda.stream(side):
+                    text_features = self.encode_text(text, normalize=True)
+                image_features = self.encode_image(image, normalize=True)
+                main.wait_stream(side)
+                text_features.record_stream(main)
             secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
         if self.output_dict:
             out = {"image_features": image_features, "text_features": text_features,

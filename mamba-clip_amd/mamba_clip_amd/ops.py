@@ -707,6 +707,12 @@ class weight_cast_scope:
 
     def __init__(self, module, dt):
         self.module, self.dt, self.active = module, dt, False
+        self.buf = None
+
+    def record_stream(self, stream):
+        """The copies are used on another stream too (ClipModel's concurrent towers)."""
+        if self.buf is not None:
+            self.buf.record_stream(stream)
 
     def __enter__(self):
         global _WCAST
@@ -723,6 +729,7 @@ class weight_cast_scope:
             plan = (key, _CastPlan(params, self.dt, params[0].device))
             _CAST_PLANS[key[:2]] = plan
         copies = plan[1].run(params)
+        self.buf = copies[0]
         _WCAST = {id(p): (p, c) for p, c in zip(params, copies)}
         self.active = True
         return self

@@ -206,7 +206,10 @@ def test_causal_conv1d_channel_major_layout():
     from mamba_clip_amd.ops import causal_conv1d
     g = torch.Generator().manual_seed(2)
     for dt in (torch.bfloat16, torch.float32):
-        for (B, D, L, K) in [(4, 96, 80, 4), (3, 16, 24, 8), (2, 24, 13, 4)]:
+        # the last three: the backward's halo kernel over several slices and 63-item wave steps, with
+        # rows of 1 and 2 vectors (every / every other neighbouring lane in another row)
+        for (B, D, L, K) in [(4, 96, 80, 4), (3, 16, 24, 8), (2, 24, 13, 4), (256, 6, 80, 4), (200, 4, 8, 4),
+                             (130, 4, 16, 4)]:
             xz = torch.randn(2 * D, B * L, generator=g).to(dt)
             w = torch.randn(D, 1, K, generator=g)
             b = torch.randn(D, generator=g)
@@ -735,3 +738,32 @@ def test_wgrad_split_k_slab_sum(M, N, K):
     ref = G.double() @ X.double()
     assert got.dtype == torch.float32 and got.shape == (N, K)
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_concurrent_towers_bitwise_identical():
+    """ClipModel runs the text tower on a second HIP stream beside the image tower: features, loss and
+    every gradient bitwise equal to the sequential forward / backward (same kernels, same order per
+    tower; autograd joins the streams)."""
+    from mamba_clip_amd.model import init_model
+    from mamba_clip_amd.loss import ClipLoss
+    torch.manual_seed(0)
+    model, _, _, _ = init_model("tiny-mamba-clip")
+    model = model.to(DEV)
+    img = torch.randn(8, 3, 32, 32, device=DEV)
+    tok = torch.randint(1, 1000, (8, 16), device=DEV)
+    runs = []
+    for conc in (True, False):
+        model.concurrent_towers = conc
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(img, tok)
+            loss = ClipLoss()(**out)["contrastive_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((out["text_features"].detach().clone(), loss.detach().clone(),
+                     {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}))
+    (tf1, l1, g1), (tf0, l0, g0) = runs
+    assert torch.equal(tf1, tf0) and torch.equal(l1, l0)
+    assert g1.keys() == g0.keys() and len(g0) > 10
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
