@@ -371,23 +371,30 @@ class ClipModel(nn.Module):
         self.context_length = getattr(self.text, "context_length", None)
         self.vocab_size = getattr(self.text, "vocab_size", None)
 
-    # image and text towers on two HIP streams (ClipModel.forward).  Off under a multi-process group:
-    # DDP launches a gradient bucket's all-reduce behind one stream, and a bucket could then hold
-    # gradients still being written on the other.
+    # image and text towers on two HIP streams (ClipModel.forward).  Under a multi-process group only
+    # when train.wrap_ddp joined the streams in its comm hook (ddp_streams_joined): DDP launches a
+    # gradient bucket's all-reduce behind one stream, and a bucket may hold gradients of both towers.
     concurrent_towers = True
+    ddp_streams_joined = False
     _side_streams = {}
+
+    @staticmethod
+    def side_stream_for(device):
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if device not in ClipModel._side_streams:
+            ClipModel._side_streams[device] = torch.cuda.Stream(device=device)
+        return ClipModel._side_streams[device]
 
     def _side_stream(self, image, text):
         if not (self.concurrent_towers and image is not None and text is not None and image.is_cuda
                 and torch.is_grad_enabled()):
             return None
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
-                and torch.distributed.get_world_size() > 1:
+                and torch.distributed.get_world_size() > 1 and not self.ddp_streams_joined:
             return None
-        dev = image.device
-        if dev not in ClipModel._side_streams:
-            ClipModel._side_streams[dev] = torch.cuda.Stream(device=dev)
-        return ClipModel._side_streams[dev]
+        return self.side_stream_for(image.device)
 
     def encode_image(self, image, normalize: bool = False):
         f = self.visual(image)

@@ -106,7 +106,25 @@ def wrap_ddp(model, args, device):
               bucket_cap_mb=getattr(args, "ddp_bucket_mb", 100))
     if device.type == "cuda":
         kw["device_ids"] = [device]
-    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+    ddp = torch.nn.parallel.DistributedDataParallel(model, **kw)
+    side = model.side_stream_for(device) if (device.type == "cuda" and hasattr(model, "side_stream_for")) else None
+    if side is not None:
+        # ClipModel runs its text tower on a second stream; a bucket may then hold gradients written
+        # on either stream, so its all-reduce is launched behind both
+        ddp.register_comm_hook((torch.cuda.current_stream(device), side), _join_streams_allreduce)
+        model.ddp_streams_joined = True
+    return ddp
+
+
+def _join_streams_allreduce(state, bucket):
+    """DDP comm hook: the launching stream waits for the main and the side stream (events at this
+    point), then the stock averaging all-reduce of the bucket."""
+    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+    cur = torch.cuda.current_stream(bucket.buffer().device)
+    for s in state:
+        if s != cur:
+            cur.wait_stream(s)
+    return default_hooks.allreduce_hook(None, bucket)
 
 
 # ---------------------------------------------------------------- one optimizer step

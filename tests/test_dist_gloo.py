@@ -238,3 +238,64 @@ def test_stage2_head_ddp_gloo_w2():
     np.testing.assert_array_equal(out[0]["grads"], out[1]["grads"])
     assert out[0]["n_train"] == out[0]["fc_numel"]           # frozen towers: only the fc head is trained
     assert np.isfinite(out[0]["grads"]).all() and np.abs(out[0]["grads"]).max() > 0
+
+
+# ---------------------------------------------------------------- DDP + two-stream towers on the GPU
+def _ddp_streams_worker(rank, world, port, q):
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+        from types import SimpleNamespace
+        import torch.distributed as dist
+        from mamba_clip_amd.loss import ClipLoss
+        from mamba_clip_amd.model import build_clip
+        from mamba_clip_amd.train import wrap_ddp
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)            # both ranks share the box's GPU (gloo moves CUDA tensors)
+        args = SimpleNamespace(distributed=True, ddp_static_graph=False, ddp_bucket_mb=1)
+        g = torch.Generator().manual_seed(5 + rank)
+        images = torch.randn(8, 3, 32, 32, generator=g).to(dev)
+        texts = torch.randint(1, 999, (8, 16), generator=g).to(dev)
+        res = {}
+        for conc in (True, False):
+            torch.manual_seed(0)
+            inner = build_clip("tiny-mamba-clip").to(dev)
+            inner.concurrent_towers = conc
+            model = wrap_ddp(inner, args, dev)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(images, texts)
+                loss = ClipLoss(rank=rank, world_size=world)(**out)["contrastive_loss"]
+            loss.backward()
+            torch.cuda.synchronize()
+            res[conc] = (torch.cat([p.grad.float().flatten() for p in inner.parameters()]).cpu().numpy(),
+                         inner.ddp_streams_joined)
+        q.put((rank, {"conc": res[True][0], "seq": res[False][0], "joined": res[True][1]}))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+@pytest.mark.gpu
+def test_ddp_two_stream_towers_gloo_gpu_w2():
+    """wrap_ddp with ClipModel's text tower on a second stream (comm hook joining the streams before
+    each bucket's all-reduce; 1 MB buckets so buckets mix both towers): all-reduced gradients
+    bitwise equal to the one-stream run, and equal on both ranks."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_streams_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["joined"]
+        np.testing.assert_array_equal(out[r]["conc"], out[r]["seq"])
+    np.testing.assert_array_equal(out[0]["conc"], out[1]["conc"])
