@@ -376,16 +376,17 @@ class ClipModel(nn.Module):
     # gradient bucket's all-reduce behind one stream, and a bucket may hold gradients of both towers.
     concurrent_towers = True
     ddp_streams_joined = False
+    side_high_priority = False   # text-tower stream at HIP's high priority (A/B toggle)
     _side_streams = {}
 
-    @staticmethod
-    def side_stream_for(device):
+    def side_stream_for(self, device):
         device = torch.device(device)
         if device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
-        if device not in ClipModel._side_streams:
-            ClipModel._side_streams[device] = torch.cuda.Stream(device=device)
-        return ClipModel._side_streams[device]
+        key = (device, bool(self.side_high_priority))
+        if key not in ClipModel._side_streams:
+            ClipModel._side_streams[key] = torch.cuda.Stream(device=device, priority=-1 if key[1] else 0)
+        return ClipModel._side_streams[key]
 
     def _side_stream(self, image, text):
         if not (self.concurrent_towers and image is not None and text is not None and image.is_cuda

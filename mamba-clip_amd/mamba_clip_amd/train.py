@@ -111,7 +111,7 @@ def wrap_ddp(model, args, device):
     if side is not None:
         # ClipModel runs its text tower on a second stream; a bucket may then hold gradients written
         # on either stream, so its all-reduce is launched behind both
-        ddp.register_comm_hook((torch.cuda.current_stream(device), side), _join_streams_allreduce)
+        ddp.register_comm_hook((torch.cuda.current_stream(device), model), _join_streams_allreduce)
         model.ddp_streams_joined = True
     return ddp
 
@@ -120,8 +120,10 @@ def _join_streams_allreduce(state, bucket):
     """DDP comm hook: the launching stream waits for the main and the side stream (events at this
     point), then the stock averaging all-reduce of the bucket."""
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-    cur = torch.cuda.current_stream(bucket.buffer().device)
-    for s in state:
+    main, model = state
+    dev = bucket.buffer().device
+    cur = torch.cuda.current_stream(dev)
+    for s in (main, model.side_stream_for(dev)):   # the side stream as the model picks it now
         if s != cur:
             cur.wait_stream(s)
     return default_hooks.allreduce_hook(None, bucket)
