@@ -136,3 +136,17 @@ def test_struct_layout_matches_header(cname, pyname):
     assert int(got["size"]) == ctypes.sizeof(cls)
     for f in fields:
         assert int(got[f]) == getattr(cls, f).offset, f
+
+
+def test_cast_chunk_layout_matches_python_table():
+    """ops._CastPlan builds the mc_cast_f32_many chunk table as int64 triples (src, dst_off, n):
+    mc_cast_chunk must be 24 B with fields at 0 / 8 / 16."""
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_ops.h"', "int main(void){",
+           'printf("%zu %zu %zu %zu\\n", sizeof(mc_cast_chunk), offsetof(mc_cast_chunk, src), '
+           'offsetof(mc_cast_chunk, dst_off), offsetof(mc_cast_chunk, n));', "return 0;}"]
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write("\n".join(src))
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
+        assert subprocess.check_output([exe]).decode().split() == ["24", "0", "8", "16"]

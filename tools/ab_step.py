@@ -25,7 +25,11 @@ ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--toggle", default="fuse_dt_proj")
+ap.add_argument("--watchdog", type=float, default=0, help="dump every thread's stack and exit after S seconds")
 args = ap.parse_args()
+if args.watchdog:
+    import faulthandler
+    faulthandler.dump_traceback_later(args.watchdog, exit=True)
 
 targs = SimpleNamespace(precision="amp_bf16", lr=5e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
                         grad_clip_norm=None, accum_freq=1, rank=0, world_size=1, distributed=False)
@@ -52,7 +56,9 @@ def run(flag, steps):
     return (time.perf_counter() - t) / steps * 1e3
 
 
+print("warmup A", flush=True)
 run(True, 3)
+print("warmup B", flush=True)
 run(False, 3)
 for r in range(args.reps):
     a = run(True, args.steps)
