@@ -389,8 +389,13 @@ class ClipModel(nn.Module):
         return ClipModel._side_streams[key]
 
     def _side_stream(self, image, text):
-        if not (self.concurrent_towers and image is not None and text is not None and image.is_cuda
-                and torch.is_grad_enabled()):
+        # only beside a Mamba text tower: the image tower's biased projections run hipBLASLt stream-K
+        # kernels, whose workgroups spin on each other and need to be co-resident.  Two such GEMMs on
+        # two streams (a ViT beside a BERT tower, C3) can each hold half the CUs and wait forever --
+        # seen as a hung C3 bench (a kernel launch blocked on a full queue).  The Mamba tower's kernels
+        # (scan, conv, norms, its plain GEMMs) never wait on other workgroups.
+        if not (self.concurrent_towers and isinstance(self.text, MambaTextEncoder) and image is not None
+                and text is not None and image.is_cuda and torch.is_grad_enabled()):
             return None
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
                 and torch.distributed.get_world_size() > 1 and not self.ddp_streams_joined:
