@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this process may run on (see _cpu_threads)")
     return ap.parse_args()
@@ -119,7 +119,7 @@ def scan_roofline(iters, warmup=10):
     torch.cuda.empty_cache()
     copy_gbs = _copy_bandwidth(dev)
     traffic, traffic_src = _pmc_traffic()
-    return {"kernel": "selective_scan_fwd (bc_relayout + scan_fwd_pair_kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
+    return {"kernel": "selective_scan_fwd (scan_fwd_pair_kernel, B/C rows read in-kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "traffic_measured_in_this_run": False,
@@ -241,8 +241,8 @@ def cpu_baseline(args, model_name):
                                         threads=threads)
     torch.set_num_threads(prev)
     return {"value": round(pps, 4), "unit": "image-text pairs/sec", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} timed fp32 CPU train steps (+1 warmup) of {model_name} at batch "
-                      f"{args.cpu_batch} via oracle/cpu_model.py ({secs:.1f} s timed)"}
+            "sample": f"median of {args.cpu_steps} timed fp32 CPU train steps (+1 warmup) of {model_name} at "
+                      f"batch {args.cpu_batch} via oracle/cpu_model.py ({secs:.1f} s timed)"}
 
 
 def cpu_baseline_scan(args):

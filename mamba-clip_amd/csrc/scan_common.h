@@ -242,6 +242,9 @@ struct FwdArgs {
   const void* dpx; const void* dpw; int rank;
   int64_t dpx_bs, dpx_ts, dpw_ds;
   void* delta_out;                   // nullable: the formed delta, strides dt_bs / dt_ds
+  // B / C rows as given (the pair kernel reads them directly; the others read the relaid bct)
+  const void* B; const void* C;
+  int64_t B_bs, B_gs, B_ns, C_bs, C_gs, C_ns;
 };
 
 int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who);

@@ -32,7 +32,7 @@ namespace mc {
 namespace scan {
 
 // FwdArgs: scan_common.h
-bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes);   // scan_fwd_pair.hip
+bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes, int itype, int wtype);   // scan_fwd_pair.hip
 int launch_fwd_pair(const FwdArgs& a, int itype, hipStream_t s);
 
 
@@ -783,12 +783,6 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
              "a mask within n_groups (got mask 0x%x, u_groups %d, n_groups %d)", p->reverse_groups, p->u_groups,
              p->n_groups);
   }
-  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
-                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
-                             p->seqlen, p->dstate, dirs ? p->reverse_groups : 0,
-                             reinterpret_cast<float*>(p->workspace), s);
-  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
-
   FwdArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
   a.n_chunks = (p->seqlen + kT - 1) / kT;
@@ -809,6 +803,9 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   a.dpx = p->delta_proj_x; a.dpw = p->delta_proj_w; a.rank = p->delta_rank;
   a.dpx_bs = p->dpx_batch_stride; a.dpx_ts = p->dpx_token_stride; a.dpw_ds = p->dpw_dim_stride;
   a.delta_out = proj ? p->delta_out : nullptr;
+  a.B = p->B; a.C = p->C;
+  a.B_bs = p->B_batch_stride; a.B_gs = p->B_group_stride; a.B_ns = p->B_dstate_stride;
+  a.C_bs = p->C_batch_stride; a.C_gs = p->C_group_stride; a.C_ns = p->C_dstate_stride;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
   const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
@@ -816,6 +813,14 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
                        vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
                        vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
                        vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
+  // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
+  // forward 0.166 vs 0.183 ms per layer).  It reads B / C rows itself: no relayout pre-pass.
+  if (!dirs && fwd_pair_ok(a, aligned, ib, p->itype, p->wtype)) return launch_fwd_pair(a, p->itype, s);
+  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
+                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
+                             p->seqlen, p->dstate, dirs ? p->reverse_groups : 0,
+                             reinterpret_cast<float*>(p->workspace), s);
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
   if (dirs) {   // per-group addressing lives in the LDS-staged kernel (vector modes: seqlen % VI == 0)
     MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta and grouped directions do not combine");
     const bool al = aligned && p->seqlen % (16 / ib) == 0;
@@ -823,9 +828,6 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
     if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
     return launch_fwd_dirs<f16_t>(a, al, s);
   }
-  // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
-  // forward 0.166 vs 0.183 ms per layer)
-  if (fwd_pair_ok(a, aligned, ib)) return launch_fwd_pair(a, p->itype, s);
   MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta needs the pair kernel's shapes (16-bit rows, "
            "dstate 16, seqlen %% 8 == 0, 16-B aligned rows, no grouped directions)");
   if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);

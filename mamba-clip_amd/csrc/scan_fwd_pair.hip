@@ -18,9 +18,13 @@
 //    pair) and their own half of B_t / C_t (two broadcast addresses per wave);
 //  * each lane writes its partial y_t over the (dt, du) bytes it consumed; the gate
 //    pass (same vector mapping as the staging, so it still holds u for D u) adds the
-//    two partials, applies silu(z) and stores 16-B vectors along the sequence.
-// Requirements (host-checked): dstate == 16, 16-B aligned 16-bit rows, seqlen % 8 == 0,
-// row spans < 2 GiB (32-bit buffer offsets), no grouped directions.
+//    two partials, applies silu(z) and stores 16-B vectors along the sequence;
+//  * B / C straight from their 16-bit rows (x_dbl slices): one 16-B vector per lane and
+//    array per chunk (state row lane & 15, positions 8 (lane >> 4) + [0, 8)), converted
+//    into the chunk's fp32 [position][B 16 | C 16] LDS block -- no fp32 pre-pass.
+// Requirements (host-checked): dstate == 16, 16-B aligned 16-bit rows (B / C too, in the
+// activation dtype), seqlen % 8 == 0, row spans < 2 GiB (32-bit buffer offsets), no
+// grouped directions.
 #include <type_traits>
 
 #include "scan_common.h"
@@ -47,9 +51,7 @@ template <typename TI, bool kSP, int kMinW, bool kPD>
 __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
   using PL = PairLayout<TI>;
   constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
-  constexpr int kBCVec = PL::kBCBytes / 16;     // float4s of one B/C chunk
-  constexpr int kBCPer = kBCVec / 64;
-  static_assert(kBCVec % 64 == 0, "B/C chunk must split evenly over the lanes");
+  static_assert(kT == 32 && kPN == 16 && VI == 8, "one 16-B B / C vector per lane and chunk");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* rowbuf = smem;
@@ -78,7 +80,15 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
   const __amdgpu_buffer_rsrc_t rs_o = rows_rsrc(a.out, a.o_bs, a.o_ds);
   const __amdgpu_buffer_rsrc_t rs_y =
       rows_rsrc(a.out_y ? a.out_y : a.u, a.out_y ? a.y_bs : a.u_bs, a.out_y ? a.y_ds : a.u_ds);
-  const __amdgpu_buffer_rsrc_t rs_bc = make_rsrc(a.bct + (int64_t)bg * L_ * (2 * kPN), (uint32_t)L_ * (2 * kPN) * 4u);
+  // B / C rows of this (batch, group): lane j reads state row j & 15, positions [8 (j >> 4), +8) of a
+  // chunk (past the end: the next row's or zero bytes -- finite, and met only by dt = du = 0 positions)
+  const __amdgpu_buffer_rsrc_t rs_B = make_rsrc(reinterpret_cast<const TI*>(a.B) + (int64_t)b * a.B_bs + (int64_t)g * a.B_gs,
+                                                (uint32_t)((15 * a.B_ns + L_) * (int64_t)sizeof(TI)));
+  const __amdgpu_buffer_rsrc_t rs_C = make_rsrc(reinterpret_cast<const TI*>(a.C) + (int64_t)b * a.C_bs + (int64_t)g * a.C_gs,
+                                                (uint32_t)((15 * a.C_ns + L_) * (int64_t)sizeof(TI)));
+  const int bcn = lane & 15, bcq = lane >> 4;
+  const uint32_t bo_B = (uint32_t)((bcn * a.B_ns + 8 * bcq) * (int64_t)sizeof(TI));
+  const uint32_t bo_C = (uint32_t)((bcn * a.C_ns + 8 * bcq) * (int64_t)sizeof(TI));
 
   // ---- projected delta: token-major dpx rows of this batch (rank values per token, 8-B pieces), the
   // wave's 32 rows of dpw; tokens past L read 0 (their delta is masked in the staging anyway)
@@ -117,16 +127,15 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
   for (int p = 0; p < kPH / 2; ++p) x[p] = f32x2{0.f, 0.f};
 
   uint4 pu[kNV], pd[kNV];
-  float4 pbc[kBCPer];
+  uint4 pB, pC;
   auto load_next = [&](int l0) {   // past the end: offsets fall outside the buffer ranges and read 0
 #pragma unroll
     for (int k = 0; k < kNV; ++k) {
       pu[k] = buf_ld16(rs_u, voff(k, a.u_ds, l0));
       if constexpr (!kPD) pd[k] = buf_ld16(rs_d, voff(k, a.dt_ds, l0));
     }
-#pragma unroll
-    for (int k = 0; k < kBCPer; ++k)
-      pbc[k] = __builtin_bit_cast(float4, buf_ld16(rs_bc, (uint32_t)(l0 * (2 * kPN) + 4 * (lane + 64 * k)) * 4u));
+    pB = buf_ld16(rs_B, bo_B + (uint32_t)l0 * (uint32_t)sizeof(TI));
+    pC = buf_ld16(rs_C, bo_C + (uint32_t)l0 * (uint32_t)sizeof(TI));
   };
 
   load_next(0);
@@ -217,8 +226,14 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
     };
     if (l0 + kT <= L_) stage(std::false_type());
     else stage(std::true_type());
+    {   // B / C chunk -> [position][B 16 | C 16] fp32 (lanes j, j + 16 share a bank: 2-way, free on ds_write_b32)
+      float* dst = bcl + (8 * bcq) * (2 * kPN) + bcn;
 #pragma unroll
-    for (int k = 0; k < kBCPer; ++k) reinterpret_cast<float4*>(bcl)[lane + 64 * k] = pbc[k];
+      for (int e = 0; e < VI; ++e) {
+        dst[e * (2 * kPN)] = elem_f<TI>(pB, e);
+        dst[e * (2 * kPN) + kPN] = elem_f<TI>(pC, e);
+      }
+    }
     wave_lds_sync();
     load_next(l0 + kT);
     uint4 cz[kNV];
@@ -336,12 +351,17 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
 }
 
 // Eligibility of the pair kernel for a (validated) forward call.
-bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes) {
+bool fwd_pair_ok(const FwdArgs& a, bool aligned, int itype_bytes, int itype, int wtype) {
   auto fits = [&](int64_t ds) {
     return ((int64_t)(kPCh - 1) * (ds < 0 ? -ds : ds) + a.seqlen) * itype_bytes < ((int64_t)1 << 31);
   };
-  return itype_bytes == 2 && aligned && a.dstate == kPN && a.seqlen % 8 == 0 && kS == kT && a.rev_groups == 0 && a.u_groups == 0 &&
-         fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) && (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds));
+  auto bc = [&](const void* t, int64_t bs, int64_t gs, int64_t ns) {   // 16-bit rows, 16-B aligned, 32-bit spans
+    return aligned16(t) && bs % 8 == 0 && gs % 8 == 0 && ns % 8 == 0 && ns >= 0 && (15 * ns + a.seqlen) * 2 < ((int64_t)1 << 31);
+  };
+  return itype_bytes == 2 && wtype == itype && aligned && a.dstate == kPN && a.seqlen % 8 == 0 && kS == kT &&
+         a.rev_groups == 0 && a.u_groups == 0 && fits(a.u_ds) && fits(a.dt_ds) && fits(a.o_ds) &&
+         (!a.z || fits(a.z_ds)) && (!a.out_y || fits(a.y_ds)) && bc(a.B, a.B_bs, a.B_gs, a.B_ns) &&
+         bc(a.C, a.C_bs, a.C_gs, a.C_ns);
 }
 
 template <typename TI, int kMinW>

@@ -17,8 +17,9 @@ SURVEY.md 8c) are defined here and random-initialised:
                      d_inner 1536, d_state 16, RMSNorm, fp32 residual stream)
   BertTextEncoder    PubMedBERT-base shape (12 x 768, ctx 256) for BiomedCLIP
 Hot ops run on the HIP library: selective scan, causal conv1d, fused
-add+RMSNorm, patch im2col, contrastive loss; dense projections are plain
-library GEMMs (hipBLASLt through torch), attention is torch SDPA.
+add+RMSNorm / add+LayerNorm, patch im2col, short-sequence attention
+(attention.hip), contrastive loss; dense projections are plain library GEMMs
+(hipBLASLt through torch, launched data-parallel: see __init__.py).
 """
 import math
 from functools import partial
@@ -26,7 +27,9 @@ from functools import partial
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+import torch.utils.checkpoint
 
+from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
                   fc1_gelu, linear_sk, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
                   weight_cast_scope, wleft_mm)
@@ -178,14 +181,28 @@ class MambaTextEncoder(nn.Module):
         # every mixer's A = -exp(A_log) in one launch (ops.NegExpManyFn)
         As = (neg_exp_many([l.mixer.A_log for l in self.layers]) if hidden.is_cuda
               else [None] * len(self.layers))
+        ckpt = self.grad_checkpointing and torch.is_grad_enabled()
         for layer, A in zip(self.layers, As):
-            hidden, residual = layer(hidden, residual, A)
+            if ckpt:   # recompute the layer in backward instead of keeping its activations
+                hidden, residual = torch.utils.checkpoint.checkpoint(layer, hidden, residual, A, use_reentrant=False)
+            else:
+                hidden, residual = layer(hidden, residual, A)
         normed, _ = add_rmsnorm(hidden, residual, self.norm_f)
         pooled = normed[:, T - 1]                                   # EOT position
         return self.proj(pooled)
 
+    grad_checkpointing = False
+
     def set_grad_checkpointing(self, enable=True):
-        self.grad_checkpointing = enable
+        """Activation checkpointing per Mamba layer (torch.utils.checkpoint, non-reentrant): the reference's
+        ClipModel.set_grad_checkpointing (model.py:1099-1102) turns it on in open_clip's towers."""
+        self.grad_checkpointing = bool(enable)
+
+
+def _run_blocks(blocks, m, h, ckpt):
+    for blk in blocks:
+        m, h = torch.utils.checkpoint.checkpoint(blk, m, h, use_reentrant=False) if ckpt else blk(m, h)
+    return m, h
 
 
 # ============================================================================ ViT-B/16 visual tower
@@ -299,8 +316,7 @@ class VisionTransformer(nn.Module):
         x = self.patch_embed(x)
         cls = self.cls_token.to(x.dtype).expand(x.shape[0], -1, -1)
         m, h = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype), None
-        for blk in self.blocks:
-            m, h = blk(m, h)
+        m, h = _run_blocks(self.blocks, m, h, self.grad_checkpointing and torch.is_grad_enabled())
         # final norm on the pooled (cls) rows only: same values as norm(x)[:, 0]
         y, _ = add_layernorm(m[:, 0], h[:, 0], self.norm.weight, self.norm.bias, self.norm.eps)
         return self.head(y)
@@ -309,8 +325,11 @@ class VisionTransformer(nn.Module):
         for p in self.parameters():
             p.requires_grad = False
 
+    grad_checkpointing = False
+
     def set_grad_checkpointing(self, enable=True):
-        self.grad_checkpointing = enable
+        """Activation checkpointing per transformer block (timm / open_clip semantics)."""
+        self.grad_checkpointing = bool(enable)
 
 
 # ============================================================================ BERT text tower (BiomedCLIP shape)
@@ -333,10 +352,15 @@ class BertTextEncoder(nn.Module):
                  ("ln.bias", self.ln.bias)],
                 [list(b.named_parameters(prefix=f"blocks.{i}")) for i, b in enumerate(self.blocks)], [])
 
+    grad_checkpointing = False
+
+    def set_grad_checkpointing(self, enable=True):
+        """Activation checkpointing per encoder layer (HF gradient_checkpointing semantics)."""
+        self.grad_checkpointing = bool(enable)
+
     def forward(self, tokens):
         m, h = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]]), None
-        for blk in self.blocks:
-            m, h = blk(m, h)
+        m, h = _run_blocks(self.blocks, m, h, self.grad_checkpointing and torch.is_grad_enabled())
         return self.proj(m[:, 0] + h[:, 0])
 
 
@@ -376,6 +400,7 @@ class ClipModel(nn.Module):
     # gradient bucket's all-reduce behind one stream, and a bucket may hold gradients of both towers.
     concurrent_towers = True
     ddp_streams_joined = False
+    last_main_stream = None
     side_high_priority = False   # text-tower stream at HIP's high priority (A/B toggle)
     _side_streams = {}
 
@@ -389,12 +414,13 @@ class ClipModel(nn.Module):
         return ClipModel._side_streams[key]
 
     def _side_stream(self, image, text):
-        # only beside a Mamba text tower: the image tower's biased projections run hipBLASLt stream-K
-        # kernels, whose workgroups spin on each other and need to be co-resident.  Two such GEMMs on
-        # two streams (a ViT beside a BERT tower, C3) can each hold half the CUs and wait forever --
-        # seen as a hung C3 bench (a kernel launch blocked on a full queue).  The Mamba tower's kernels
-        # (scan, conv, norms, its plain GEMMs) never wait on other workgroups.
-        if not (self.concurrent_towers and isinstance(self.text, MambaTextEncoder) and image is not None
+        # Only when no kernel of either tower waits on another workgroup of its launch: our HIP kernels
+        # never do, and the library GEMMs do not when hipBLASLt launches them data-parallel (one
+        # workgroup per output tile, GEMM_GRIDS_DATA_PARALLEL).  Its default stream-K
+        # grids split tiles over workgroups that wait on each other's partial sums, so two of them on
+        # two streams can each hold part of the CUs and wait forever (the round-3 C3 hang); the C2
+        # Mamba tower ran such split launches too (tools/sk_probe.sh).
+        if not (self.concurrent_towers and GEMM_GRIDS_DATA_PARALLEL and image is not None
                 and text is not None and image.is_cuda and torch.is_grad_enabled()):
             return None
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
@@ -424,6 +450,7 @@ class ClipModel(nn.Module):
                 # beside the image tower (its backward follows it there: autograd runs each backward op
                 # on its forward op's stream and joins the streams at the end of backward)
                 main = torch.cuda.current_stream()
+                self.last_main_stream = main                 # train._join_streams_allreduce joins it
                 side.wait_stream(main)                       # the one-launch weight casts, the inputs
                 text.record_stream(side)
                 casts.record_stream(side)
@@ -463,6 +490,7 @@ class ClipModel(nn.Module):
                 p.requires_grad = (not freeze_layer_norm) if _is_norm_param(n) else False
 
     def set_grad_checkpointing(self, enable=True):
+        """model.py:1099-1102: both towers recompute their blocks / layers in backward."""
         for t in (self.visual, self.text):
             if hasattr(t, "set_grad_checkpointing"):
                 t.set_grad_checkpointing(enable)

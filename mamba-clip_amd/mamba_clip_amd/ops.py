@@ -813,18 +813,19 @@ class WeightLeftMM(torch.autograd.Function):
             dw = wgrad(g, Xc.t())
         acc = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[1]:
-            if acc is not None and Xc.stride(1) == 1 and Xc.is_contiguous():
+            accv = acc.transpose(0, 1) if (acc is not None and Xc.is_contiguous()) else None
+            accv = accv.view(Xc.shape) if (accv is not None and accv.is_contiguous()
+                                           and accv.numel() == Xc.numel()) else None
+            if accv is not None:
                 # the other consumer's gradient (GradHandoff), in X's layout: dX += w^T g in the epilogue
-                dX = acc.transpose(0, 1).reshape(Xc.shape)
-                if dX.data_ptr() != acc.data_ptr() or not dX.is_contiguous():
-                    raise RuntimeError("wleft_mm backward: handed-off gradient is not in X's layout")
+                dX = accv
                 dX.addmm_(wc.t(), g)
                 acc = None
             elif Xc.stride(0) == 1 and Xc.stride(1) != 1:
                 dX = torch.mm(g.t(), wc).t()      # X is a transposed view: keep its layout (no copy downstream)
             else:
                 dX = torch.mm(wc.t(), g)
-            if acc is not None:
+            if acc is not None:   # handed-off gradient in another layout: summed after the GEMM
                 dX = dX + acc.transpose(0, 1).reshape(Xc.shape)
         return dw, dX, None
 

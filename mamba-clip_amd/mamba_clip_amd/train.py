@@ -106,8 +106,17 @@ def wrap_ddp(model, args, device):
               bucket_cap_mb=getattr(args, "ddp_bucket_mb", 100))
     if device.type == "cuda":
         kw["device_ids"] = [device]
-    ddp = torch.nn.parallel.DistributedDataParallel(model, **kw)
     side = model.side_stream_for(device) if (device.type == "cuda" and hasattr(model, "side_stream_for")) else None
+    if side is not None and hasattr(model, "text"):
+        # DDP keeps every parameter's AccumulateGrad node alive from here on, and a node runs on the
+        # stream current at its creation.  Created now on the main stream, each text-tower gradient
+        # would make the main stream wait for the side stream's backward at that point (autograd's
+        # stream-mismatch sync), serialising the towers again; created under the side stream, the
+        # text tower's gradients are accumulated (and DDP's bucket copies made) where they are produced.
+        with torch.cuda.stream(side):
+            model._side_grad_accumulators = [p.view_as(p).grad_fn.next_functions[0][0]
+                                             for p in model.text.parameters() if p.requires_grad]
+    ddp = torch.nn.parallel.DistributedDataParallel(model, **kw)
     if side is not None:
         # ClipModel runs its text tower on a second stream; a bucket may then hold gradients written
         # on either stream, so its all-reduce is launched behind both
@@ -117,16 +126,31 @@ def wrap_ddp(model, args, device):
 
 
 def _join_streams_allreduce(state, bucket):
-    """DDP comm hook: the launching stream waits for the main and the side stream (events at this
-    point), then the stock averaging all-reduce of the bucket."""
+    """DDP comm hook: the launching stream waits for the forward's main stream and the side stream
+    (events at this point), then the stock averaging all-reduce of the bucket.  Both streams are
+    resolved at call time: the main one as the last forward recorded it, the side one as the model
+    picks it now (the wrap-time stream is only the fallback)."""
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-    main, model = state
+    main_at_wrap, model = state
     dev = bucket.buffer().device
-    cur = torch.cuda.current_stream(dev)
-    for s in (main, model.side_stream_for(dev)):   # the side stream as the model picks it now
-        if s != cur:
-            cur.wait_stream(s)
-    return default_hooks.allreduce_hook(None, bucket)
+    main = getattr(model, "last_main_stream", None) or main_at_wrap
+    # the join happens on a third stream: neither tower's stream is held up waiting for the other
+    join = _comm_join_stream(dev)
+    join.wait_stream(main)
+    join.wait_stream(model.side_stream_for(dev))
+    bucket.buffer().record_stream(join)
+    with torch.cuda.stream(join):
+        return default_hooks.allreduce_hook(None, bucket)
+
+
+_JOIN_STREAMS = {}
+
+
+def _comm_join_stream(dev):
+    key = torch.device(dev)
+    if key not in _JOIN_STREAMS:
+        _JOIN_STREAMS[key] = torch.cuda.Stream(device=key)
+    return _JOIN_STREAMS[key]
 
 
 # ---------------------------------------------------------------- one optimizer step

@@ -89,8 +89,9 @@ def oracle_clip_loss(image_features, text_features, logit_scale, output_dict=Tru
     return {"contrastive_loss": loss} if output_dict else loss
 
 
-def cpu_train_pairs_per_sec(model_name="vit_b16-mamba130m", batch=8, steps=2, warmup=1, threads=None, seed=0):
-    """fp32 CPU fwd+bwd+AdamW steps of the same architecture; returns (pairs/s, seconds timed)."""
+def cpu_train_pairs_per_sec(model_name="vit_b16-mamba130m", batch=8, steps=5, warmup=1, threads=None, seed=0):
+    """fp32 CPU fwd+bwd+AdamW steps of the same architecture; returns (pairs/s from the MEDIAN step
+    time, seconds timed in total) -- the median of `steps` timed steps, as BASELINE.md plans."""
     from mamba_clip_amd.data import synthetic_batch
     from mamba_clip_amd.model import build_clip
     if threads:
@@ -111,11 +112,14 @@ def cpu_train_pairs_per_sec(model_name="vit_b16-mamba130m", batch=8, steps=2, wa
                 model.logit_scale.clamp_(0, 4.605170185988092)
         for _ in range(warmup):
             step()
-        t0 = time.perf_counter()
+        times = []
         for _ in range(steps):
+            t0 = time.perf_counter()
             step()
-        dt = time.perf_counter() - t0
-    return batch * steps / dt, dt
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2] if len(times) % 2 else 0.5 * (times[len(times) // 2 - 1] + times[len(times) // 2])
+    return batch / med, sum(times)
 
 
 def cpu_scan_gbps(batch=1, dim=3072, seqlen=4096, dstate=16, threads=None, seed=0):

@@ -236,3 +236,23 @@ def test_vssm_tiny_cpu_restatement_matches_reference_golden():
     cols = torch.nn.functional.unfold(img, 4, stride=4).transpose(1, 2).reshape(-1, 48)
     back = PatchIm2colFn.backward(type("C", (), {"meta": (2, 3, 8, 12, 4)})(), cols)[0]
     assert torch.equal(back, img)
+
+
+def test_gemm_grids_data_parallel_gate():
+    """Importing the package asks hipBLASLt for data-parallel GEMM grids; the two-stream
+    towers are gated on it: with the variable preset to anything but 1 the gate is off and ClipModel
+    keeps both towers on one stream."""
+    import os
+    import subprocess
+    import sys
+    import mamba_clip_amd
+    assert os.environ["TENSILE_STREAMK_DATA_PARALLEL"] == "1"
+    assert mamba_clip_amd.GEMM_GRIDS_DATA_PARALLEL
+    code = ("import mamba_clip_amd, mamba_clip_amd.model as m; "
+            "print(mamba_clip_amd.GEMM_GRIDS_DATA_PARALLEL, m.GEMM_GRIDS_DATA_PARALLEL)")
+    env = dict(os.environ, TENSILE_STREAMK_DATA_PARALLEL="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = os.path.join(root, "mamba-clip_amd") + os.pathsep + env.get("PYTHONPATH", "")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["False", "False"]

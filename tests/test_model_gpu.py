@@ -740,14 +740,24 @@ def test_wgrad_split_k_slab_sum(M, N, K):
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
-def test_concurrent_towers_bitwise_identical():
-    """ClipModel runs the text tower on a second HIP stream beside the image tower: features, loss and
-    every gradient bitwise equal to the sequential forward / backward (same kernels, same order per
-    tower; autograd joins the streams)."""
-    from mamba_clip_amd.model import init_model
+@pytest.mark.parametrize("text_tower", ["mamba", "bert"])
+def test_concurrent_towers_bitwise_identical(text_tower):
+    """ClipModel runs the text tower on a second HIP stream beside the image tower -- beside a Mamba
+    tower (C2) and beside a BERT tower (C3), whose library GEMMs now also run concurrently with the
+    ViT's (data-parallel grids, mamba_clip_amd.GEMM_GRIDS_DATA_PARALLEL): features, loss and every
+    gradient bitwise equal to the sequential forward / backward (same kernels, same order per tower;
+    autograd joins the streams)."""
+    import mamba_clip_amd
+    from mamba_clip_amd.model import BertTextEncoder, ClipModel, VisionTransformer, init_model
     from mamba_clip_amd.loss import ClipLoss
+    assert mamba_clip_amd.GEMM_GRIDS_DATA_PARALLEL
     torch.manual_seed(0)
-    model, _, _, _ = init_model("tiny-mamba-clip")
+    if text_tower == "mamba":
+        model, _, _, _ = init_model("tiny-mamba-clip")
+    else:
+        model = ClipModel(VisionTransformer(img_size=32, patch=8, width=64, layers=2, heads=4, output_dim=32),
+                          BertTextEncoder(vocab_size=1000, context_length=16, width=64, layers=2, heads=4,
+                                          output_dim=32))
     model = model.to(DEV)
     img = torch.randn(8, 3, 32, 32, device=DEV)
     tok = torch.randint(1, 1000, (8, 16), device=DEV)
@@ -762,6 +772,7 @@ def test_concurrent_towers_bitwise_identical():
         torch.cuda.synchronize()
         runs.append((out["text_features"].detach().clone(), loss.detach().clone(),
                      {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}))
+        del out, loss   # no graph (and no AccumulateGrad node) survives into the next run
     (tf1, l1, g1), (tf0, l0, g0) = runs
     assert torch.equal(tf1, tf0) and torch.equal(l1, l0)
     assert g1.keys() == g0.keys() and len(g0) > 10
