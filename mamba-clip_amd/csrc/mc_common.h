@@ -183,6 +183,10 @@ __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off
 __device__ __forceinline__ void buf_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off, 0, 0);
 }
+// streaming (non-temporal, nt cache policy) store: the line is not kept in L2 for re-use
+__device__ __forceinline__ void buf_st16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off, 0, 2);
+}
 // elements [0, nvalid) of a 16-B vector (nvalid wave-uniform)
 template <typename T>
 __device__ __forceinline__ void buf_st16_masked(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& q, int nvalid) {

@@ -211,6 +211,23 @@ __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
   else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(s), "v"(c));
   return r;
 }
+// exp2 of two values on the packed-FMA pipe (no transcendental): round-to-nearest split x = j + f
+// with the 1.5 * 2^23 shifter, a degree-6 near-minimax polynomial for 2^f on [-0.5, 0.5] (relative
+// error 9.6e-8), j added into the exponent field.  For x in [-126, 126].  A/B lever for the forward
+// recurrence (MC_FWD_POLY_PAIRS, scan_fwd_pair.hip): 15 VALU ops for two values against two v_exp_f32.
+__device__ __forceinline__ f32x2 exp2_poly2(f32x2 x) {
+  x = f32x2{fmaxf(x.x, -126.f), fmaxf(x.y, -126.f)};
+  const f32x2 t = x + 12582912.f;
+  const f32x2 f = x - (t - 12582912.f);
+  f32x2 p = f * 1.534579787403345e-4f + 1.3399930903688073e-3f;
+  p = p * f + 9.618489071726799e-3f;
+  p = p * f + 5.550328642129898e-2f;
+  p = p * f + 2.4022646248340607e-1f;
+  p = p * f + 6.931471824645996e-1f;
+  p = p * f + 1.f;
+  return f32x2{__int_as_float(__float_as_int(p.x) + (__float_as_int(t.x) << 23)),
+               __int_as_float(__float_as_int(p.y) + (__float_as_int(t.y) << 23))};
+}
 __device__ __forceinline__ f32x2 silu2(f32x2 z) {
   const f32x2 arg = z * -kLog2e;
   const f32x2 ep = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)} + 1.f;

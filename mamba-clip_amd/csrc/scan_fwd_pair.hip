@@ -36,6 +36,16 @@ constexpr int kPCh = 32;   // channels per wave
 constexpr int kPN = 16;    // dstate
 constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
+// State pairs per lane whose decays use the packed-FMA exp2 polynomial instead of v_exp_f32 (A/B
+// lever, VERDICT r03: balance the transcendental and the packed pipes).  Measured slower: 0.
+#ifndef MC_FWD_POLY_PAIRS
+#define MC_FWD_POLY_PAIRS 0
+#endif
+// Output rows stored non-temporally (A/B lever: keep L2 for the u / delta / z lines whose second
+// 64-B half the next chunk reads)
+#ifndef MC_FWD_NT_STORE
+#define MC_FWD_NT_STORE 0
+#endif
 
 template <typename TI>
 struct PairLayout {
@@ -273,7 +283,8 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
             // dt broadcast from its half of the {dt, dt} register pair
             const f32x2 arg = (e & 1) ? pk_mul_bcast<1>(A2[p], e < 2 ? q0.xy : q1.xy)
                                       : pk_mul_bcast<0>(A2[p], e < 2 ? q0.xy : q1.xy);
-            dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+            if (p < MC_FWD_POLY_PAIRS) dA[p] = exp2_poly2(arg);   // A/B lever (default 0: all v_exp_f32)
+            else dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
           }
           {   // du broadcast from its half of {du, du}
             const f32x2 dup = e < 2 ? q0.zw : q1.zw;
@@ -338,7 +349,8 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           o[e + 1] = g.y;
         }
       }
-      buf_st16(rs_o, voff(k, a.o_ds, l0) | ob, pack_f<TI>(o));
+      if constexpr (MC_FWD_NT_STORE) buf_st16_nt(rs_o, voff(k, a.o_ds, l0) | ob, pack_f<TI>(o));
+      else buf_st16(rs_o, voff(k, a.o_ds, l0) | ob, pack_f<TI>(o));
     }
     wave_lds_sync();   // next chunk's staging overwrites the rows
   }

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MAMBA_CLIP_AMD_LIB overrides the path (dev A/B builds only)
-LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB", os.path.join(_HERE, "libmamba_clip_amd.so"))
+LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB") or os.path.join(_HERE, "libmamba_clip_amd.so")
 
 MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3 = 0, 1, 2, 3
 MC_SCAN_CHUNK = 32

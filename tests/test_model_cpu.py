@@ -256,3 +256,27 @@ def test_gemm_grids_data_parallel_gate():
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.split() == ["False", "False"]
+
+
+def test_grad_checkpointing_recomputes_same_gradients_cpu():
+    """ClipModel.set_grad_checkpointing (reference model.py:1099-1102) recomputes every ViT block and
+    Mamba layer in backward: same loss and gradients as without it (CPU restatement ops)."""
+    from oracle.cpu_model import oracle_clip_loss, oracle_ops
+    torch.manual_seed(0)
+    model, _, _, _ = init_model("tiny-mamba-clip")
+    img = torch.randn(4, 3, 32, 32)
+    tok = torch.randint(1, 1000, (4, 16))
+    res = []
+    for ck in (False, True):
+        model.set_grad_checkpointing(ck)
+        assert model.visual.grad_checkpointing == ck and model.text.grad_checkpointing == ck
+        model.zero_grad(set_to_none=True)
+        with oracle_ops():
+            loss = oracle_clip_loss(**model(img, tok))["contrastive_loss"]
+            loss.backward()
+        res.append((loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}))
+    (l0, g0), (l1, g1) = res
+    torch.testing.assert_close(l1, l0, rtol=0, atol=0)
+    assert g0.keys() == g1.keys() and len(g0) > 10
+    for n in g0:
+        torch.testing.assert_close(g1[n], g0[n], rtol=1e-6, atol=1e-7, msg=n)

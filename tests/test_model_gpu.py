@@ -778,3 +778,35 @@ def test_concurrent_towers_bitwise_identical(text_tower):
     assert g1.keys() == g0.keys() and len(g0) > 10
     for n in g0:
         assert torch.equal(g1[n], g0[n]), n
+
+
+@pytest.mark.parametrize("conc", [False, True])
+def test_grad_checkpointing_bitwise_gpu(conc):
+    """Per-block / per-layer activation checkpointing on the HIP path (also with the text tower on its
+    side stream, where the recompute runs during that stream's backward): gradients bitwise equal to
+    the run that keeps the activations (deterministic kernels recompute identical values)."""
+    from mamba_clip_amd.model import init_model
+    from mamba_clip_amd.loss import ClipLoss
+    torch.manual_seed(0)
+    model, _, _, _ = init_model("tiny-mamba-clip")
+    model = model.to(DEV)
+    model.concurrent_towers = conc
+    img = torch.randn(8, 3, 32, 32, device=DEV)
+    tok = torch.randint(1, 1000, (8, 16), device=DEV)
+    runs = []
+    for ck in (False, True):
+        model.set_grad_checkpointing(ck)
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(img, tok)
+            loss = ClipLoss()(**out)["contrastive_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((loss.detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                             if p.grad is not None}))
+        del out, loss
+    (l0, g0), (l1, g1) = runs
+    assert torch.equal(l0, l1)
+    assert g0.keys() == g1.keys() and len(g0) > 10
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n

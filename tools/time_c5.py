@@ -34,7 +34,7 @@ for name, fn in (("fp8 fp32-out", lambda: gemm_nt(qi, qt, alpha_dev=scale, scale
 try:
     a8 = qi[:, :e].contiguous()
     b8 = qt[:, :e].contiguous().t()
-    for od in (torch.bfloat16,):
+    for od in (torch.bfloat16, torch.float32):
         fn = lambda: torch._scaled_mm(a8, b8, scale_a=si.view(-1, 1), scale_b=st.view(1, -1), out_dtype=od)  # noqa: E731
         for _ in range(3):
             fn()
@@ -46,6 +46,7 @@ try:
         t.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(t) / 20
-        print(f"torch._scaled_mm (hipBLASLt) {od}: {ms * 1e3:.1f} us  {2 * n * n * e / ms / 1e9:.0f} TFLOP/s")
+        print(f"torch._scaled_mm (hipBLASLt, TENSILE_STREAMK_DATA_PARALLEL={os.environ.get('TENSILE_STREAMK_DATA_PARALLEL')}) "
+              f"{od}: {ms * 1e3:.1f} us  {2 * n * n * e / ms / 1e9:.0f} TFLOP/s")
 except Exception as ex:  # noqa: BLE001
     print("torch._scaled_mm unavailable:", repr(ex)[:200])
