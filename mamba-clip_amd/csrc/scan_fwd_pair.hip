@@ -37,14 +37,17 @@ constexpr int kPN = 16;    // dstate
 constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
 // State pairs per lane whose decays use the packed-FMA exp2 polynomial instead of v_exp_f32 (A/B
-// lever, VERDICT r03: balance the transcendental and the packed pipes).  Measured slower: 0.
+// lever, VERDICT r03: balance the transcendental and the packed pipes).  Measured: one pair of four
+// 3.20 ms, two 3.79 ms against 2.56-2.86 ms (profiles/r04/scan_fwd_exp_poly_ab.txt) -- v_exp_f32 does
+// not co-issue with the packed FMAs, and the polynomial costs 15 issue slots per two values: 0.
 #ifndef MC_FWD_POLY_PAIRS
 #define MC_FWD_POLY_PAIRS 0
 #endif
-// Output rows stored non-temporally (A/B lever: keep L2 for the u / delta / z lines whose second
-// 64-B half the next chunk reads)
+// Output rows stored non-temporally (nt cache policy): L2 keeps the u / delta / z lines whose second
+// 64-B half the next chunk reads.  Interleaved C4 A/B 2.81-2.84 vs 2.83-2.86 ms; PMC writes 1.58 GB
+// (= the output) instead of 1.85 GB, reads 4.35 vs 4.56 GB raw (profiles/r04/scan_fwd_nt_store_ab.txt)
 #ifndef MC_FWD_NT_STORE
-#define MC_FWD_NT_STORE 0
+#define MC_FWD_NT_STORE 1
 #endif
 
 template <typename TI>
