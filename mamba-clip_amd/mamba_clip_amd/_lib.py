@@ -123,6 +123,43 @@ class AttnBwdParams(ctypes.Structure):
     ]
 
 
+class SS2DConvParams(ctypes.Structure):
+    """Mirror of ``mc_ss2d_conv_params`` (include/mc_ss2d.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("height", c_i32), ("width", c_i32), ("channels", c_i32), ("ksize", c_i32),
+        ("xtype", c_i32), ("x_batch_stride", c_i64), ("x_row_stride", c_i64), ("x_col_stride", c_i64),
+        ("x", c_vp), ("weight", c_fp), ("bias", c_fp), ("u", c_fp),
+    ]
+
+
+class SS2DConvBwdParams(ctypes.Structure):
+    """Mirror of ``mc_ss2d_conv_bwd_params`` (include/mc_ss2d.h)."""
+    _fields_ = [
+        ("fwd", SS2DConvParams), ("du", c_fp), ("dx", c_vp), ("dweight", c_fp), ("dbias", c_fp),
+        ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class SS2DMergeParams(ctypes.Structure):
+    """Mirror of ``mc_ss2d_merge_params`` (include/mc_ss2d.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("height", c_i32), ("width", c_i32), ("channels", c_i32),
+        ("ztype", c_i32), ("ytype", c_i32), ("eps", ctypes.c_float),
+        ("out", c_fp), ("z", c_vp), ("z_batch_stride", c_i64), ("z_row_stride", c_i64), ("z_col_stride", c_i64),
+        ("ln_weight", c_fp), ("ln_bias", c_fp), ("y", c_vp), ("mean", c_fp), ("rstd", c_fp),
+    ]
+
+
+class SS2DMergeBwdParams(ctypes.Structure):
+    """Mirror of ``mc_ss2d_merge_bwd_params`` (include/mc_ss2d.h)."""
+    _fields_ = [
+        ("fwd", SS2DMergeParams), ("dy", c_vp),
+        ("dy_batch_stride", c_i64), ("dy_row_stride", c_i64), ("dy_col_stride", c_i64),
+        ("dout", c_fp), ("dz", c_vp), ("dln_weight", c_fp), ("dln_bias", c_fp),
+        ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -171,6 +208,12 @@ SYMBOLS = {
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),
+    "mc_ss2d_conv_stack_fwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvParams), c_vp]),
+    "mc_ss2d_conv_stack_bwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvBwdParams), c_vp]),
+    "mc_ss2d_conv_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
+    "mc_ss2d_merge_ln_gate_fwd": (ctypes.c_int, [ctypes.POINTER(SS2DMergeParams), c_vp]),
+    "mc_ss2d_merge_ln_gate_bwd": (ctypes.c_int, [ctypes.POINTER(SS2DMergeBwdParams), c_vp]),
+    "mc_ss2d_merge_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
 }
 
 _lib = None

@@ -32,7 +32,7 @@ import torch.utils.checkpoint
 from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
                   fc1_gelu, linear_sk, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
-                  weight_cast_scope, wleft_mm)
+                  ss2d_conv_stack, ss2d_merge_ln_gate, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
@@ -638,41 +638,40 @@ class SS2D(nn.Module):
         self.out_proj = nn.Linear(di, d_model, bias=bias)
         self.dropout = nn.Dropout(dropout) if dropout > 0.0 else None
 
-    def _scan_dirs(self, x):  # (B, d, H, W) -> (B, 4, d, L) outputs, directions in their own frames
-        """model.py:503-565 with the flips inside the scan kernel's addressing: u = [x, x^T] is the only
-        copy (the reference stacks [x, x^T, flip x, flip x^T]); the per-direction projections read it
-        in place; directions 2 / 3 walk u blocks 0 / 1 backwards (grouped_scan_fn), so their outputs
-        come back un-flipped.  Blocks 1 / 3 are still in the transposed (W, H) frame."""
-        Bsz, d, H, W = x.shape
-        L, K = H * W, 4
-        u = torch.stack([x.reshape(Bsz, d, L), x.transpose(2, 3).reshape(Bsz, d, L)], dim=1)   # (B, 2, d, L)
+    def _scan_u(self, u):  # u = [x, x^T] (B, 2, d, L) fp32 -> (B, 4 d, L), directions in their own frames
+        """model.py:503-565 with the cross-scan inside the kernels: u holds x and x^T once (the
+        reference stacks [x, x^T, flip x, flip x^T]); the per-direction projections read it in place;
+        directions 2 / 3 walk u blocks 0 / 1 backwards (grouped_scan_fn), so their outputs come back
+        un-flipped.  Blocks 1 / 3 stay in the transposed (W, H) frame: the merge reads them there."""
+        Bsz, _, d, L = u.shape
+        K = 4
         w = self.x_proj_weight.to(u.dtype).view(2, 2, -1, d)                # [i][j]: direction k = 2 i + j
         x_dbl = torch.einsum("bjdl,ijcd->bijcl", u, w).reshape(Bsz, K, -1, L)
         dts, Bs, Cs = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=2)
         dts = torch.einsum("bkrl,kdr->bkdl", dts, self.dt_projs_weight.to(u.dtype))
-        out = grouped_scan_fn(u.float().reshape(Bsz, 2 * d, L), dts.float().reshape(Bsz, K * d, L),
-                              -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
-                              self.dt_projs_bias.float().reshape(-1), delta_softplus=True,
-                              reverse_groups=SS2D_REVERSE_GROUPS, u_groups=SS2D_U_GROUPS)
-        return out.view(Bsz, K, d, L)
+        return grouped_scan_fn(u.float().reshape(Bsz, 2 * d, L), dts.float().reshape(Bsz, K * d, L),
+                               -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
+                               self.dt_projs_bias.float().reshape(-1), delta_softplus=True,
+                               reverse_groups=SS2D_REVERSE_GROUPS, u_groups=SS2D_U_GROUPS)
 
     def forward_core(self, x):  # (B, d, H, W) -> four (B, d, L) maps, fp32, reference order
+        """The reference's forward_corev0 contract (model.py:503-565) on a conv output: y1 .. y4 back in
+        the (H, W) frame.  Not on the forward path (forward fuses the stack and the merge)."""
         Bsz, d, H, W = x.shape
-        out = self._scan_dirs(x)
-        back = lambda t: t.reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, H * W)  # noqa: E731
+        L = H * W
+        u = torch.stack([x.reshape(Bsz, d, L), x.transpose(2, 3).reshape(Bsz, d, L)], dim=1).float()
+        out = self._scan_u(u).view(Bsz, 4, d, L)
+        back = lambda t: t.reshape(Bsz, d, W, H).transpose(2, 3).reshape(Bsz, d, L)  # noqa: E731
         return out[:, 0], out[:, 2], back(out[:, 1]), back(out[:, 3])
 
     def forward(self, x, **kwargs):  # (B, H, W, C)
-        Bsz, H, W, _ = x.shape
+        # model.py:630-647.  x / z stay channels-last halves of in_proj's output (no permute copy);
+        # ss2d_conv_stack writes silu(conv2d(x)) straight into the scan input u = [x, x^T] (fp32), and
+        # ss2d_merge_ln_gate sums the four directions (the two column-major ones read transposed),
+        # applies out_norm and the silu(z) gate, channels-last for out_proj (mc_ss2d.h)
         x, z = self.in_proj(x).chunk(2, dim=-1)
-        x = self.act(self.conv2d(x.permute(0, 3, 1, 2).contiguous()))
-        out = self._scan_dirs(x)
-        d = out.shape[2]
-        # merge (model.py:553-565, 643): one transpose back for the two column-major directions
-        y_t = (out[:, 1] + out[:, 3]).view(Bsz, d, W, H)
-        y = (out[:, 0] + out[:, 2]).view(Bsz, d, H, W) + y_t.transpose(2, 3)
-        y = y.permute(0, 2, 3, 1)
-        y = self.out_norm(y) * F.silu(z)
+        u = ss2d_conv_stack(x, self.conv2d.weight, self.conv2d.bias)
+        y = ss2d_merge_ln_gate(self._scan_u(u), z, self.out_norm.weight, self.out_norm.bias, self.out_norm.eps)
         out = self.out_proj(y)
         return self.dropout(out) if self.dropout is not None else out
 

@@ -12,6 +12,8 @@
                           materialised S (kept for logits the caller needs anyway).
 All launches go on the current HIP stream; nothing synchronises.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -1021,3 +1023,135 @@ class PackedAttentionFn(torch.autograd.Function):
 
 def packed_attention(qkv, heads):
     return PackedAttentionFn.apply(qkv, heads)
+
+
+# ---------------------------------------------------------------------------- SS2D cross-scan glue (mc_ss2d.h)
+def _cl_ok(t):
+    """Channels-last view the SS2D kernels take as is: unit channel stride, 4-element aligned."""
+    return (t.stride(-1) == 1 and t.shape[-1] % 4 == 0 and all(s % 4 == 0 for s in t.stride()[:3])
+            and t.data_ptr() % (4 * t.element_size()) == 0)
+
+
+class SS2DConvStackFn(torch.autograd.Function):
+    """u = [x, x^T] of SS2D's cross-scan, fp32 (B, 2, C, H*W), from the channels-last in_proj half:
+    silu(depthwise conv3x3(x) + b) written in both frames by one kernel (reference model.py:636-637
+    permute + conv2d + SiLU, 510-517 stack / transpose, 531-537 fp32 cast)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        if not x.is_cuda:
+            raise RuntimeError("ss2d_conv_stack: CUDA tensors only (the CPU restatement lives in oracle/)")
+        Bsz, H, W, C = x.shape
+        k = weight.shape[-1]
+        xs = x if _cl_ok(x) else x.contiguous()
+        w32 = weight.float().contiguous()
+        b32 = bias.float().contiguous() if bias is not None else None
+        u = torch.empty(Bsz, 2, C, H * W, device=x.device, dtype=torch.float32)
+        p = _lib.SS2DConvParams()
+        p.batch, p.height, p.width, p.channels, p.ksize = Bsz, H, W, C, k
+        p.xtype = _lib.dtype_code(xs.dtype)
+        p.x_batch_stride, p.x_row_stride, p.x_col_stride = xs.stride(0), xs.stride(1), xs.stride(2)
+        p.x, p.weight, p.bias, p.u = xs.data_ptr(), w32.data_ptr(), _lib.ptr(b32), u.data_ptr()
+        _lib.check(_lib.load().mc_ss2d_conv_stack_fwd(ctypes.byref(p), _lib.stream_handle(x.device)),
+                   "mc_ss2d_conv_stack_fwd")
+        ctx.save_for_backward(xs, w32, b32)
+        ctx.dtypes = (weight.dtype, bias.dtype if bias is not None else None)
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        xs, w32, b32 = ctx.saved_tensors
+        Bsz, H, W, C = xs.shape
+        k = w32.shape[-1]
+        du = du.float().contiguous()
+        dx = torch.empty(Bsz, H, W, C, device=xs.device, dtype=xs.dtype)
+        dw = torch.empty_like(w32)
+        db = torch.empty(C, device=xs.device, dtype=torch.float32) if b32 is not None else None
+        lib = _lib.load()
+        ws_b = lib.mc_ss2d_conv_bwd_workspace_bytes(Bsz, H, W, C, k)
+        ws = _ws(ws_b, xs.device)
+        p = _lib.SS2DConvBwdParams()
+        f = p.fwd
+        f.batch, f.height, f.width, f.channels, f.ksize = Bsz, H, W, C, k
+        f.xtype = _lib.dtype_code(xs.dtype)
+        f.x_batch_stride, f.x_row_stride, f.x_col_stride = xs.stride(0), xs.stride(1), xs.stride(2)
+        f.x, f.weight, f.bias = xs.data_ptr(), w32.data_ptr(), _lib.ptr(b32)
+        p.du, p.dx, p.dweight, p.dbias = du.data_ptr(), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db)
+        p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+        _lib.check(lib.mc_ss2d_conv_stack_bwd(ctypes.byref(p), _lib.stream_handle(xs.device)), "mc_ss2d_conv_stack_bwd")
+        wdt, bdt = ctx.dtypes
+        return dx, dw.to(wdt), db.to(bdt) if db is not None else None
+
+
+def ss2d_conv_stack(x, weight, bias):
+    return SS2DConvStackFn.apply(x, weight, bias)
+
+
+class SS2DMergeFn(torch.autograd.Function):
+    """y = LayerNorm(((y1 + y2) + y3) + y4) * silu(z), channels-last, from the grouped scan's
+    (B, 4C, H*W) fp32 output (directions 1 / 3 in the x^T frame) -- reference model.py:553-565 flips /
+    transposes and 640-643 sum, transpose, out_norm, gate -- in one kernel; the backward writes each
+    direction's output gradient in its own frame, dz and the LayerNorm parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, out, z, ln_w, ln_b, eps, y_dtype):
+        if not out.is_cuda:
+            raise RuntimeError("ss2d_merge_ln_gate: CUDA tensors only (the CPU restatement lives in oracle/)")
+        Bsz, H, W, C = z.shape
+        o = out.float().contiguous()
+        zs = z if _cl_ok(z) else z.contiguous()
+        lw = ln_w.float().contiguous()
+        lb = ln_b.float().contiguous() if ln_b is not None else None
+        y = torch.empty(Bsz, H, W, C, device=out.device, dtype=y_dtype)
+        mean = torch.empty(Bsz * H * W, device=out.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        p = _lib.SS2DMergeParams()
+        _merge_params(p, o, zs, lw, lb, eps, y_dtype, mean, rstd)
+        p.y = y.data_ptr()
+        _lib.check(_lib.load().mc_ss2d_merge_ln_gate_fwd(ctypes.byref(p), _lib.stream_handle(out.device)),
+                   "mc_ss2d_merge_ln_gate_fwd")
+        ctx.save_for_backward(o, zs, lw, lb, mean, rstd)
+        ctx.cfg = (eps, y_dtype, z.dtype, ln_w.dtype, ln_b.dtype if ln_b is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        o, zs, lw, lb, mean, rstd = ctx.saved_tensors
+        eps, y_dtype, z_dt, lw_dt, lb_dt = ctx.cfg
+        Bsz, H, W, C = zs.shape
+        dy = dy.to(y_dtype)
+        if not _cl_ok(dy):
+            dy = dy.contiguous()
+        dout = torch.empty_like(o)
+        dz = torch.empty(Bsz, H, W, C, device=zs.device, dtype=zs.dtype)
+        dlw = torch.empty_like(lw)
+        dlb = torch.empty_like(lb) if lb is not None else None
+        lib = _lib.load()
+        ws_b = lib.mc_ss2d_merge_bwd_workspace_bytes(Bsz, H, W, C)
+        ws = _ws(ws_b, zs.device)
+        p = _lib.SS2DMergeBwdParams()
+        _merge_params(p.fwd, o, zs, lw, lb, eps, y_dtype, mean, rstd)
+        p.dy = dy.data_ptr()
+        p.dy_batch_stride, p.dy_row_stride, p.dy_col_stride = dy.stride(0), dy.stride(1), dy.stride(2)
+        p.dout, p.dz, p.dln_weight, p.dln_bias = dout.data_ptr(), dz.data_ptr(), dlw.data_ptr(), _lib.ptr(dlb)
+        p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+        _lib.check(lib.mc_ss2d_merge_ln_gate_bwd(ctypes.byref(p), _lib.stream_handle(zs.device)),
+                   "mc_ss2d_merge_ln_gate_bwd")
+        return (dout, dz.to(z_dt), dlw.to(lw_dt), dlb.to(lb_dt) if dlb is not None else None, None, None)
+
+
+def _merge_params(p, o, zs, lw, lb, eps, y_dtype, mean, rstd):
+    Bsz, H, W, C = zs.shape
+    p.batch, p.height, p.width, p.channels = Bsz, H, W, C
+    p.ztype, p.ytype, p.eps = _lib.dtype_code(zs.dtype), _lib.dtype_code(y_dtype), float(eps)
+    p.out, p.z = o.data_ptr(), zs.data_ptr()
+    p.z_batch_stride, p.z_row_stride, p.z_col_stride = zs.stride(0), zs.stride(1), zs.stride(2)
+    p.ln_weight, p.ln_bias = lw.data_ptr(), _lib.ptr(lb)
+    p.mean, p.rstd = mean.data_ptr(), rstd.data_ptr()
+
+
+def ss2d_merge_ln_gate(out, z, ln_weight, ln_bias, eps):
+    """out (B, 4C, H*W) fp32, z (B, H, W, C) channels-last -> (B, H, W, C): fp32 like the reference's
+    LayerNorm output, or the autocast dtype under autocast (the value out_proj's cast would give)."""
+    y_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+    return SS2DMergeFn.apply(out, z, ln_weight, ln_bias, eps, y_dtype)

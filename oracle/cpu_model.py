@@ -1,7 +1,7 @@
 """CPU restatement of the stage-1 training step (TEST / BASELINE INFRASTRUCTURE ONLY).
 
 Used by bench.py's `cpu_baseline` leg and by tests: the SAME module classes
-as the product (mamba_clip_amd.model), with their five HIP entry points
+as the product (mamba_clip_amd.model), with their HIP entry points
 swapped for the fp32 CPU restatements of this directory while the context is
 active, and the loss computed by oracle/loss_ref.clip_loss (loss.py:89-147).
 This is the "reference's CPU path" of SURVEY.md 8(d): fp32 PyTorch-CPU eager,
@@ -62,12 +62,35 @@ def grouped_scan_ref(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=
     return torch.stack([fl(out[:, g], g) for g in range(G)], 1).reshape(Bsz, dim, L)
 
 
+def ss2d_conv_stack_ref(x, weight, bias):
+    """SS2D's conv front and cross-scan input the way the reference builds it (model.py:636-637:
+    permute + depthwise conv2d + SiLU; 510-517: stack [x, x^T]; 531-537: fp32): (B, 2, C, H*W)."""
+    xc = x.permute(0, 3, 1, 2)
+    k = weight.shape[-1]
+    y = F.silu(F.conv2d(xc, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None, padding=k // 2,
+                        groups=xc.shape[1]))
+    Bsz, C, H, W = y.shape
+    return torch.stack([y.reshape(Bsz, C, H * W), y.transpose(2, 3).reshape(Bsz, C, H * W)], dim=1).float()
+
+
+def ss2d_merge_ln_gate_ref(out, z, ln_weight, ln_bias, eps):
+    """The reference merge (model.py:553-565: directions 1 / 3 transposed back; 640-643: y1 + y2 + y3 +
+    y4, transpose, out_norm, * silu(z)) on the grouped scan's (B, 4C, H*W) output."""
+    Bsz, H, W, C = z.shape
+    o = out.view(Bsz, 4, C, H * W)
+    back = lambda t: t.reshape(Bsz, C, W, H).transpose(2, 3).reshape(Bsz, C, H * W)  # noqa: E731
+    y = o[:, 0] + o[:, 2] + back(o[:, 1]) + back(o[:, 3])
+    y = y.transpose(1, 2).reshape(Bsz, H, W, C)
+    return F.layer_norm(y, (C,), ln_weight, ln_bias, eps) * F.silu(z)
+
+
 def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None):
     return selective_scan_ref(x, delta, A, Bm, Cm, D, z=z, delta_bias=delta_bias, delta_softplus=True)
 
 
 _OPS = {"selective_scan_fn": selective_scan_ref, "mixer_scan": _mixer_scan, "grouped_scan_fn": grouped_scan_ref, "add_rmsnorm": _add_rmsnorm_f32,
-        "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col, "add_layernorm": _add_layernorm_f32}
+        "causal_conv1d": _causal_conv1d_f32, "patch_im2col": _im2col, "add_layernorm": _add_layernorm_f32,
+        "ss2d_conv_stack": ss2d_conv_stack_ref, "ss2d_merge_ln_gate": ss2d_merge_ln_gate_ref}
 
 
 @contextmanager

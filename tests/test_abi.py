@@ -115,13 +115,17 @@ def test_attention_validation_without_launch():
                                           ("mc_ce_fused_params", "CEFusedParams"),
                                           ("mc_qkv_pack_params", "QkvPackParams"),
                                           ("mc_attn_fwd_params", "AttnFwdParams"),
-                                          ("mc_attn_bwd_params", "AttnBwdParams")])
+                                          ("mc_attn_bwd_params", "AttnBwdParams"),
+                                          ("mc_ss2d_conv_params", "SS2DConvParams"),
+                                          ("mc_ss2d_conv_bwd_params", "SS2DConvBwdParams"),
+                                          ("mc_ss2d_merge_params", "SS2DMergeParams"),
+                                          ("mc_ss2d_merge_bwd_params", "SS2DMergeBwdParams")])
 def test_struct_layout_matches_header(cname, pyname):
     from mamba_clip_amd import _lib
     cls = getattr(_lib, pyname)
     fields = [f for f, _ in cls._fields_]
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', '#include "mc_contrastive.h"',
-           '#include "mc_ops.h"', '#include "mc_attn.h"',
+           '#include "mc_ops.h"', '#include "mc_attn.h"', '#include "mc_ss2d.h"',
            "int main(void){",
            f'printf("size %zu\\n", sizeof({cname}));']
     src += [f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields]
