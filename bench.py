@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="pairs per GPU")
     ap.add_argument("--model", default="vit_b16-mamba130m")
     ap.add_argument("--scan-iters", type=int, default=20)
+    ap.add_argument("--input", choices=["resident", "host"], default="resident",
+                    help="resident: one synthetic batch in HBM (the `value` definition); host: ISIC-shaped raw "
+                         "uint8 crops streamed from pinned host memory each step (data.HostToDeviceLoader)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
@@ -292,9 +295,26 @@ def main():
     images, texts, targets = synthetic_batch(args.batch, 224, inner.text.context_length, inner.text.vocab_size,
                                              device=device, seed=1000 + rank)
     model.train()
+    if args.input == "host":
+        # each rank streams its own shard: 8 batches of raw crops, cycled epoch after epoch
+        from mamba_clip_amd.data import HostToDeviceLoader, IsicShapedDataset
+        shard = IsicShapedDataset(8 * args.batch, 224, inner.text.context_length, inner.text.vocab_size,
+                                  seed=1000 + rank)
+        loader = HostToDeviceLoader(shard, args.batch, device, seed=rank)
 
-    def step():
-        return train_step(model, images, texts, targets, loss, optimizer, None, targs)
+        def batches():
+            epoch = 0
+            while True:
+                loader.set_epoch(epoch)
+                yield from loader
+                epoch += 1
+        feed = batches()
+
+        def step():
+            return train_step(model, *next(feed), loss, optimizer, None, targs)
+    else:
+        def step():
+            return train_step(model, images, texts, targets, loss, optimizer, None, targs)
 
     for _ in range(args.warmup):
         losses = step()
@@ -336,10 +356,13 @@ def main():
         "median_ms_per_step": round(median_ms, 3),
         "median_pairs_per_sec": round(world * args.batch / (median_ms * 1e-3), 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": f"synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) {seq_len}-token text, EOT last)",
+        "data": (f"synthetic (random-init weights; N(0,1) 224x224 images, U[1,vocab) {seq_len}-token text, EOT last)"
+                 if args.input == "resident" else
+                 f"synthetic ISIC-shaped shard streamed from pinned host memory each step (raw 224x224x3 uint8 "
+                 f"crops normalised on the GPU, U[1,vocab) {seq_len}-token text; random-init weights)"),
         "config": {"workload": workload,
                    "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                   "seq_len": seq_len, "image_size": 224,
+                   "seq_len": seq_len, "image_size": 224, "input": args.input,
                    "parallelism": f"dp{world}",
                    "library_gemm_selection": "tunableop-file" if gemm_tuned else "default-heuristic"},
         "mfma_estimate": {"flop_per_pair": flop_pair,
@@ -348,6 +371,8 @@ def main():
                           "frac": round(value / world * flop_pair / 1e12 / MFMA_BF16_DENSE_TFLOPS, 4)},
         "final_loss": round(final_loss, 5),
     }
+    if args.input == "host":
+        feed.close()                              # joins the loader's host thread
     del images, texts, targets, optimizer
     torch.cuda.empty_cache()
     if rank == 0 and not args.no_roofline:

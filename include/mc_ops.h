@@ -12,6 +12,8 @@
  *                           sequence of (batch, dim, seqlen) activations, the
  *                           short conv in front of the scan (the 2-D analogue is
  *                           SS2D's depthwise conv, model.py:331-339)
+ *   mc_patch_embed_input     the image input path: float NCHW or raw uint8 NHWC images ->
+ *                           normalised patch rows for the patch-embed GEMM in one pass
  *   mc_patch_im2col          ViT / VSSM patch-embed input reshuffle: stride ==
  *                           kernel conv as a GEMM (model.py:189-191 PatchEmbed2D)
  * Same conventions as mc_scan.h: device pointers, caller-owned buffers,
@@ -80,6 +82,23 @@ size_t mc_causal_conv1d_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t 
  * img (batch, C, H, W) contiguous; H % P == W % P == 0; same dtype in and out. */
 int mc_patch_im2col(int32_t batch, int32_t C, int32_t H, int32_t W, int32_t P, int32_t dtype, const void* img,
                     void* patches, void* stream);
+
+/* The image input path of the patch embedding (reference: data.py get_transform 37-108 ToTensor +
+ * Normalize, then the visual tower's k = s = P patch conv):
+ *   out[(b*ph + i)*pw + j, (c*P + ky)*P + kx] = scale[c] * img(b, c, i*P + ky, j*P + kx) + shift[c]
+ * img: float NCHW (f32 / bf16 / f16; scale, shift nullable -> a plain im2col with a dtype cast) or
+ * uint8 NHWC decoded images (1 or 3 channels; scale = 1 / (255 std), shift = -mean / std).
+ * P % 4 == 0, H % P == W % P == 0; out (B*ph*pw, C*P*P) row-major in out_dtype (f32 / bf16 / f16). */
+enum { MC_LAYOUT_NCHW = 0, MC_LAYOUT_NHWC = 1 };
+typedef struct mc_patch_input_params {
+  int32_t batch, channels, height, width, patch;
+  int32_t layout, in_dtype, out_dtype;
+  const void* img;
+  const float* scale;   /* (C,) fp32, nullable together with shift */
+  const float* shift;
+  void* out;
+} mc_patch_input_params;
+int mc_patch_embed_input(const mc_patch_input_params* p, void* stream);
 
 /* Fused gradient passes that also produce the bias gradient of the GEMM in
  * front of them, in the same single stream over the (rows x cols) gradient

@@ -39,7 +39,8 @@ typedef enum mc_dtype {
   MC_DTYPE_F32 = 0,
   MC_DTYPE_BF16 = 1,
   MC_DTYPE_F16 = 2,
-  MC_DTYPE_FP8_E4M3 = 3  /* OCP e4m3fn (gfx950 native fp8); contrastive GEMM operands only */
+  MC_DTYPE_FP8_E4M3 = 3, /* OCP e4m3fn (gfx950 native fp8); contrastive GEMM operands only */
+  MC_DTYPE_U8 = 4         /* raw decoded image bytes; mc_patch_embed_input only */
 } mc_dtype;
 
 enum {

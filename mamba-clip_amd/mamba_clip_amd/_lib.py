@@ -11,7 +11,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MAMBA_CLIP_AMD_LIB overrides the path (dev A/B builds only)
 LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB") or os.path.join(_HERE, "libmamba_clip_amd.so")
 
-MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3 = 0, 1, 2, 3
+MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3, MC_DTYPE_U8 = 0, 1, 2, 3, 4
+MC_LAYOUT_NCHW, MC_LAYOUT_NHWC = 0, 1
 MC_SCAN_CHUNK = 32
 MC_SCAN_MAX_DSTATE = 32
 MC_CAST_CHUNK = 16384
@@ -160,6 +161,15 @@ class SS2DMergeBwdParams(ctypes.Structure):
     ]
 
 
+class PatchInputParams(ctypes.Structure):
+    """Mirror of ``mc_patch_input_params`` (include/mc_ops.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("channels", c_i32), ("height", c_i32), ("width", c_i32), ("patch", c_i32),
+        ("layout", c_i32), ("in_dtype", c_i32), ("out_dtype", c_i32),
+        ("img", c_vp), ("scale", c_fp), ("shift", c_fp), ("out", c_vp),
+    ]
+
+
 # symbol -> (restype, argtypes); every entry point include/*.h declares
 SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
@@ -208,6 +218,7 @@ SYMBOLS = {
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),
+    "mc_patch_embed_input": (ctypes.c_int, [ctypes.POINTER(PatchInputParams), c_vp]),
     "mc_ss2d_conv_stack_fwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvParams), c_vp]),
     "mc_ss2d_conv_stack_bwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvBwdParams), c_vp]),
     "mc_ss2d_conv_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
@@ -247,9 +258,9 @@ def check(rc, what):
 def dtype_code(dt):
     import torch
     codes = {torch.float32: MC_DTYPE_F32, torch.bfloat16: MC_DTYPE_BF16, torch.float16: MC_DTYPE_F16,
-             torch.float8_e4m3fn: MC_DTYPE_FP8_E4M3}
+             torch.float8_e4m3fn: MC_DTYPE_FP8_E4M3, torch.uint8: MC_DTYPE_U8}
     if dt not in codes:
-        raise RuntimeError(f"mamba_clip_amd: unsupported dtype {dt} (float32, bfloat16, float16, float8_e4m3fn only)")
+        raise RuntimeError(f"mamba_clip_amd: unsupported dtype {dt} (float32, bfloat16, float16, float8_e4m3fn, uint8 only)")
     return codes[dt]
 
 

@@ -22,6 +22,7 @@ add+RMSNorm / add+LayerNorm, patch im2col, short-sequence attention
 (hipBLASLt through torch, launched data-parallel: see __init__.py).
 """
 import math
+import os
 from functools import partial
 
 import torch
@@ -214,10 +215,12 @@ class PatchEmbed(nn.Module):
         self.patch, self.grid = patch, img_size // patch
         self.proj = nn.Conv2d(in_chans, dim, patch, patch, bias=bias)
 
-    def forward(self, x):  # (B, C, H, W) -> (B, H/P * W/P, dim)
+    def forward(self, x):  # (B, C, H, W) float, or (B, H, W, C) uint8 raw images -> (B, H/P * W/P, dim)
         Bsz = x.shape[0]
-        dt = x.dtype if not torch.is_autocast_enabled("cuda") else torch.get_autocast_dtype("cuda")
-        cols = patch_im2col(x.to(dt), self.patch)
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else (
+            torch.float32 if x.dtype == torch.uint8 else x.dtype)
+        # the input cast (and for raw images ToTensor + Normalize) happens inside the patch kernel
+        cols = patch_im2col(x, self.patch, dt)
         w = self.proj.weight.reshape(self.proj.weight.shape[0], -1)
         if cols.is_cuda:   # split-K weight gradient (ops.wgrad): 188 -> 85 us at C2
             out = linear_sk(cols, w, self.proj.bias)
@@ -398,7 +401,7 @@ class ClipModel(nn.Module):
     # image and text towers on two HIP streams (ClipModel.forward).  Under a multi-process group only
     # when train.wrap_ddp joined the streams in its comm hook (ddp_streams_joined): DDP launches a
     # gradient bucket's all-reduce behind one stream, and a bucket may hold gradients of both towers.
-    concurrent_towers = True
+    concurrent_towers = os.environ.get("MAMBA_CLIP_AMD_CONCURRENT_TOWERS", "1") != "0"
     ddp_streams_joined = False
     last_main_stream = None
     side_high_priority = False   # text-tower stream at HIP's high priority (A/B toggle)
@@ -572,9 +575,11 @@ class PatchEmbed2D(nn.Module):
         self.proj = nn.Conv2d(in_chans, embed_dim, self.patch, self.patch)
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
 
-    def forward(self, x):
-        Bsz, _, H, W = x.shape
-        cols = patch_im2col(x, self.patch)
+    def forward(self, x):  # (B, C, H, W) float, or (B, H, W, C) uint8 raw images
+        Bsz, H, W = (x.shape[0], x.shape[1], x.shape[2]) if x.dtype == torch.uint8 else (x.shape[0], x.shape[2], x.shape[3])
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else (
+            torch.float32 if x.dtype == torch.uint8 else x.dtype)
+        cols = patch_im2col(x, self.patch, dt)
         w = self.proj.weight.reshape(self.proj.weight.shape[0], -1).to(cols.dtype)
         y = F.linear(cols, w, self.proj.bias.to(cols.dtype)).reshape(Bsz, H // self.patch, W // self.patch, -1)
         return self.norm(y) if self.norm is not None else y

@@ -531,32 +531,72 @@ def causal_conv1d(x, weight, bias=None, silu=True, dx_slab=None):
     return CausalConv1dFn.apply(x, weight, bias, silu, dx_slab)
 
 
+# open_clip's OPENAI_DATASET_MEAN / _STD: the reference's default Normalize (data.py:47-53)
+IMAGE_MEAN = (0.48145466, 0.4578275, 0.40821073)
+IMAGE_STD = (0.26862954, 0.26130258, 0.27577711)
+_NORM_CACHE = {}
+
+
+def _norm_affine(device, C, mean, std):
+    """scale = 1 / (255 std), shift = -mean / std per channel (ToTensor + Normalize on raw bytes)."""
+    key = (device, C, tuple(mean), tuple(std))
+    if key not in _NORM_CACHE:
+        m = torch.tensor(mean, dtype=torch.float64)[:C]
+        sd = torch.tensor(std, dtype=torch.float64)[:C]
+        _NORM_CACHE[key] = ((1.0 / (255.0 * sd)).float().to(device), (-m / sd).float().to(device))
+    return _NORM_CACHE[key]
+
+
 class PatchIm2colFn(torch.autograd.Function):
-    """Non-overlapping (k = s = P) patch rows.  The map is a permutation of the image, so the
-    backward is the inverse permutation (one strided copy): VSSM's input gradient
-    (model.py:189-201) flows through it."""
+    """Non-overlapping (k = s = P) patch rows in `out_dtype`, the input cast fused in (float NCHW), or
+    the whole image input path for raw uint8 NHWC images (ToTensor + Normalize + patchify,
+    mc_patch_embed_input).  For a float image the map is a permutation, so the backward is the inverse
+    permutation (one strided copy): VSSM's input gradient (model.py:189-201) flows through it."""
 
     @staticmethod
-    def forward(ctx, img, patch):
+    def forward(ctx, img, patch, out_dtype, mean, std):
         lib = _lib.load()
+        u8 = img.dtype == torch.uint8
         img = img.contiguous()
-        Bsz, C, H, W = img.shape
-        out = torch.empty(Bsz * (H // patch) * (W // patch), C * patch * patch, device=img.device, dtype=img.dtype)
-        _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(img.dtype), img.data_ptr(),
-                                       out.data_ptr(), _lib.stream_handle(img.device)), "mc_patch_im2col")
-        ctx.meta = (Bsz, C, H, W, patch)
+        if u8:
+            Bsz, H, W, C = img.shape
+        else:
+            Bsz, C, H, W = img.shape
+        out_dtype = out_dtype or (torch.float32 if u8 else img.dtype)
+        out = torch.empty(Bsz * (H // patch) * (W // patch), C * patch * patch, device=img.device, dtype=out_dtype)
+        if patch % 4 == 0:
+            p = _lib.PatchInputParams()
+            p.batch, p.channels, p.height, p.width, p.patch = Bsz, C, H, W, patch
+            p.layout = _lib.MC_LAYOUT_NHWC if u8 else _lib.MC_LAYOUT_NCHW
+            p.in_dtype, p.out_dtype = _lib.dtype_code(img.dtype), _lib.dtype_code(out_dtype)
+            if u8:
+                sc, sh = _norm_affine(img.device, C, mean or IMAGE_MEAN, std or IMAGE_STD)
+                p.scale, p.shift = sc.data_ptr(), sh.data_ptr()
+            p.img, p.out = img.data_ptr(), out.data_ptr()
+            _lib.check(lib.mc_patch_embed_input(ctypes.byref(p), _lib.stream_handle(img.device)), "mc_patch_embed_input")
+        else:   # VSSM's P = 4 goes here too; other P (not a multiple of 4): element-wise kernel, same dtype
+            if u8:
+                raise RuntimeError("patch_im2col: uint8 images need a patch size that is a multiple of 4")
+            src = img if img.dtype == out_dtype else img.to(out_dtype)
+            _lib.check(lib.mc_patch_im2col(Bsz, C, H, W, patch, _lib.dtype_code(out_dtype), src.data_ptr(),
+                                           out.data_ptr(), _lib.stream_handle(img.device)), "mc_patch_im2col")
+        ctx.meta = (Bsz, C, H, W, patch, img.dtype)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        Bsz, C, H, W, P = ctx.meta
+        Bsz, C, H, W, P, in_dt = ctx.meta
+        if in_dt == torch.uint8:
+            return None, None, None, None, None
         gi = g.reshape(Bsz, H // P, W // P, C, P, P).permute(0, 3, 1, 4, 2, 5).reshape(Bsz, C, H, W)
-        return gi, None
+        return gi.to(in_dt), None, None, None, None
 
 
-def patch_im2col(img, patch):
-    """(B, C, H, W) -> (B * H/P * W/P, C * P * P) patch rows (row = (b, h/P, w/P), col = (c, ph, pw))."""
-    return PatchIm2colFn.apply(img, patch)
+def patch_im2col(img, patch, out_dtype=None, mean=None, std=None):
+    """(B, C, H, W) float -> (B * H/P * W/P, C * P * P) patch rows (row = (b, h/P, w/P), col = (c, ph, pw)),
+    cast to out_dtype on the way; or (B, H, W, C) uint8 raw images -> the same rows normalised with
+    mean / std (default open_clip's OPENAI_DATASET_MEAN / _STD, the reference's transform)."""
+    return PatchIm2colFn.apply(img, patch, out_dtype, mean, std)
 
 
 # ---------------------------------------------------------------------------- projections with split-K weight grads

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .data import normalize_images
 from .utils.amp_utils import get_autocast, get_input_dtype
 from .utils.dist_utils import is_master
 
@@ -64,6 +65,8 @@ def get_model_inputs(args, images, texts, targets=None, balanced_images=None, ba
     """train.py:66-89: optional balanced mixup, then (images,) or (images, texts)."""
     if getattr(args, "balanced_mixup", None):
         lam = np.random.beta(a=args.balanced_mixup, b=1)
+        if images.dtype == torch.uint8:   # raw crops: mix the normalised images (the reference mixes those)
+            images, balanced_images = normalize_images(images), normalize_images(balanced_images)
         images = (1 - lam) * images + lam * balanced_images
         if lam > 0.5 and texts is not None and balanced_texts is not None:
             texts = balanced_texts
@@ -200,8 +203,14 @@ def _balanced_to(balanced, device, input_dtype):
     if balanced is None:
         return None
     img, txt, tgt = balanced
-    return (img.to(device=device, dtype=input_dtype), txt.to(device=device) if txt is not None else None,
+    return (_images_to(img, device, input_dtype), txt.to(device=device) if txt is not None else None,
             tgt.to(device=device))
+
+
+def _images_to(images, device, input_dtype):
+    """Float batches take the input dtype; raw uint8 crops stay bytes (normalised in the patch kernel)."""
+    dt = input_dtype if images.is_floating_point() else None
+    return images.to(device=device, dtype=dt, non_blocking=True)
 
 
 def train_step(model, images, texts, targets, loss, optimizer, scaler, args, autocast=None, balanced=None):
@@ -280,7 +289,7 @@ def train_one_epoch(model, data, loss, epoch, optimizer, scaler, scheduler, args
             scheduler(step)
         images, texts, targets, balanced = split_batch(batch, getattr(args, "balanced_mixup", None))
         balanced = _balanced_to(balanced, device, input_dtype)
-        images = images.to(device=device, dtype=input_dtype, non_blocking=True)
+        images = _images_to(images, device, input_dtype)
         texts = texts.to(device=device, non_blocking=True) if texts is not None else None
         targets = targets.to(device=device, non_blocking=True)
         data_time_m.update(time.time() - end)

@@ -14,7 +14,9 @@ import tempfile
 import torch
 
 _DIR = os.path.dirname(os.path.abspath(__file__))
-DEFAULT_FILE = os.path.join(_DIR, "gemm_gfx950_c2_b256.csv")
+# C2 (b 256) and C3 (b 64) shapes, measured with the data-parallel grids the package sets
+# (tools/tune_gemms.sh); MAMBA_CLIP_AMD_GEMM_TUNING_FILE overrides (A/B runs)
+DEFAULT_FILE = os.environ.get("MAMBA_CLIP_AMD_GEMM_TUNING_FILE") or os.path.join(_DIR, "gemm_gfx950_dp.csv")
 
 
 def load_gemm_tuning(path=DEFAULT_FILE):

@@ -36,9 +36,25 @@ def _add_layernorm_f32(x, res, w, b, eps=1e-6):
     return y.to(x.dtype), h
 
 
-def _im2col(img, P):
+IMAGE_MEAN = (0.48145466, 0.4578275, 0.40821073)   # open_clip OPENAI_DATASET_MEAN / _STD (data.py:47-53)
+IMAGE_STD = (0.26862954, 0.26130258, 0.27577711)
+
+
+def to_tensor_normalize(img_u8, mean=IMAGE_MEAN, std=IMAGE_STD):
+    """The reference's ToTensor + Normalize (data.py:102-106) on a (B, H, W, C) uint8 batch -> NCHW fp32."""
+    C = img_u8.shape[-1]
+    x = img_u8.permute(0, 3, 1, 2).double() / 255.0
+    m = torch.tensor(mean[:C], dtype=torch.float64).view(1, C, 1, 1)
+    s = torch.tensor(std[:C], dtype=torch.float64).view(1, C, 1, 1)
+    return ((x - m) / s).float()
+
+
+def _im2col(img, P, out_dtype=None, mean=None, std=None):
+    if img.dtype == torch.uint8:
+        img = to_tensor_normalize(img, mean or IMAGE_MEAN, std or IMAGE_STD)
     B, C, H, W = img.shape
-    return F.unfold(img, P, stride=P).transpose(1, 2).reshape(B * (H // P) * (W // P), C * P * P)
+    cols = F.unfold(img, P, stride=P).transpose(1, 2).reshape(B * (H // P) * (W // P), C * P * P)
+    return cols.to(out_dtype) if out_dtype is not None else cols
 
 
 def grouped_scan_ref(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=False, reverse_groups=0,

@@ -234,7 +234,7 @@ def test_vssm_tiny_cpu_restatement_matches_reference_golden():
     # the product im2col's backward is the exact inverse permutation of the unfold layout
     img = torch.randn(2, 3, 8, 12, dtype=torch.float64)
     cols = torch.nn.functional.unfold(img, 4, stride=4).transpose(1, 2).reshape(-1, 48)
-    back = PatchIm2colFn.backward(type("C", (), {"meta": (2, 3, 8, 12, 4)})(), cols)[0]
+    back = PatchIm2colFn.backward(type("C", (), {"meta": (2, 3, 8, 12, 4, torch.float64)})(), cols)[0]
     assert torch.equal(back, img)
 
 
