@@ -33,6 +33,12 @@
 namespace mc {
 namespace scan {
 
+#ifndef MC_BWD_EXP_NORECOMP
+#define MC_BWD_EXP_NORECOMP 0
+#endif
+#ifndef MC_BWD_EXP_NOY
+#define MC_BWD_EXP_NOY 0
+#endif
 constexpr int kQW = 4;            // waves per workgroup
 constexpr int kQCh = 32;          // channels per wave
 constexpr int kQN = 16;           // dstate
@@ -369,6 +375,14 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
     wave_lds_sync();
 
     // ---- recompute pass: states at the starts of sub-tiles 1 .. nsub - 1 -> LDS
+#if MC_BWD_EXP_NORECOMP   // timing experiment only: states of sub-tile starts read from HBM instead (wrong values)
+    for (int s = 0; s + 1 < nsub; ++s) {
+      const uint32_t ox = ((uint32_t)my_r * cs_row + (uint32_t)(min(c * 4 + s, a.n_states - 1) * kQN + 8 * h)) * 4u;
+      xst[(2 * s) * 64 + lane] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox));
+      xst[(2 * s + 1) * 64 + lane] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox + 16));
+    }
+    if (0)
+#endif
     {
       f32x2 x[kQP];
 #pragma unroll
@@ -468,7 +482,9 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
             if (t > 0) qn = bquad(kQT * s + t - 1, p);
             lam = (t & 1) ? pk_fma_bcast<1>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha)
                           : pk_fma_bcast<0>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha);
+#if !MC_BWD_EXP_NOY
             if (hasZ) Y2[t] = q.hi * xs[t] + Y2[t];
+#endif
             S2[t] = lam * q.lo + S2[t];
             red[t] = (t & 1) ? pk_mul_bcast<1>(lam, sc.dtu[t >> 1]) : pk_mul_bcast<0>(lam, sc.dtu[t >> 1]);
             ha = lam * as[t];
@@ -499,7 +515,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
       }
       float fY[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) fY[e] = pair_finish(Y2[e], Y2[4 + e], h);
+      for (int e = 0; e < 4; ++e) fY[e] = MC_BWD_EXP_NOY ? 0.f : pair_finish(Y2[e], Y2[4 + e], h);
       float o_du[4], o_dd[4], o_dz[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {

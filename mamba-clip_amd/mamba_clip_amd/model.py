@@ -85,7 +85,7 @@ class MambaMixer(nn.Module):
         # dt_proj inside the scan (ProjectedScanFn) where the shapes allow.  Off by default: the scan
         # kernels are VALU-bound, so forming delta on their MFMAs costs more than the delta stream it
         # saves (C2 step 88.4 vs 86.5 ms on one box, profiles/r03/c2_ab_fuse_dt_proj.txt)
-        self.fuse_dt_proj = False
+        self.fuse_dt_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_DT_PROJ", "0") == "1"   # A/B toggle
         self.du_handoff = True   # scan du -> x_proj's dX epilogue (ops.GradHandoff)
 
     def forward(self, hidden, A=None):  # (B, L, d_model) contiguous; A: -exp(A_log) when the tower formed it

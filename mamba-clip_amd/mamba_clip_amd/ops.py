@@ -92,10 +92,23 @@ def similarity_fp8(image_features, text_features, logit_scale, out_dtype=torch.f
     """
     qi, si = quant_rows_fp8(image_features)
     qt, st = quant_rows_fp8(text_features)
+    if out_dtype == torch.bfloat16 and _rowwise_scaled_mm_ok(qi, qt):
+        # bf16 logits: hipBLASLt's row-wise scaled fp8 GEMM (torch._scaled_mm) measured faster than
+        # sim_fp8_kernel at C5 (59.7-60.4 vs 86.4 us, profiles/r04/c5_variants_dp.txt); alpha folds into
+        # the row factors.  hipBLASLt has no fp32-out row-wise kernel: fp32 logits stay on sim_fp8_kernel.
+        sa = (si * (logit_scale.reshape(()).float() if torch.is_tensor(logit_scale) else float(logit_scale)))
+        return torch._scaled_mm(qi, qt.t(), scale_a=sa.reshape(-1, 1), scale_b=st.reshape(1, -1),
+                                out_dtype=torch.bfloat16)
     if torch.is_tensor(logit_scale):
         return gemm_nt(qi, qt, alpha_dev=logit_scale.reshape(()).float().contiguous(), out_dtype=out_dtype,
                        scale_a=si, scale_b=st)
     return gemm_nt(qi, qt, alpha=float(logit_scale), out_dtype=out_dtype, scale_a=si, scale_b=st)
+
+
+def _rowwise_scaled_mm_ok(qi, qt):
+    """Shapes hipBLASLt's row-wise fp8 kernels take (K % 16, N % 16: qt.t() column-major, 16-B rows)."""
+    return (hasattr(torch, "_scaled_mm") and qi.shape[1] == qt.shape[1] and qi.shape[1] % 16 == 0
+            and qt.shape[0] % 16 == 0 and qi.shape[0] > 0)
 
 
 def clip_loss_fp8(image_features, text_features, logit_scale):

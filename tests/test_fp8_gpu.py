@@ -99,6 +99,10 @@ def test_similarity_fp8_c5_size_properties():
     d = torch.diagonal(S)
     assert (d - 100.0).abs().max() <= 2.0                        # |q(x)|^2 ~ 1 within the fp8 bound
     assert torch.equal(S.argmax(dim=1).cpu(), torch.arange(8192))
+    # bf16 logits (shipped on hipBLASLt's row-wise fp8 GEMM): the fp32 kernel's values within bf16 rounding
+    Sb = similarity_fp8(I, I, torch.tensor(100.0, device=DEV), out_dtype=torch.bfloat16)
+    assert Sb.dtype == torch.bfloat16 and Sb.shape == S.shape
+    assert float((Sb.float() - S).abs().max()) <= 2 ** -8 * float(S.abs().max()) + 1e-3
 
 
 def test_clip_model_get_logits_fp8():
