@@ -62,6 +62,8 @@ enum {
  * inside a chunk from the one saved at its start.  32 positions = 2 B per
  * (channel, position) at dstate 16, a quarter of the bf16 activations. */
 #define MC_SCAN_CHUNK 32
+/* the fine saved-state interval (mc_scan_fwd_params.state_interval) */
+#define MC_SCAN_STATE_INTERVAL_FINE 8
 
 typedef struct mc_scan_fwd_params {
   int32_t batch, dim, seqlen, dstate, n_groups;
@@ -123,6 +125,16 @@ typedef struct mc_scan_fwd_params {
   int32_t delta_rank;
   int64_t dpx_batch_stride, dpx_token_stride, dpw_dim_stride;
   void* delta_out;
+  /* Saved-state interval of a training call: chunk_states holds the state after
+   * every state_interval positions (and after the last position), i.e.
+   * mc_scan_n_states(seqlen, state_interval) entries per channel.  0 or
+   * MC_SCAN_CHUNK (32): the default.  MC_SCAN_STATE_INTERVAL_FINE (8): the
+   * backward reads the state entering each of its 8-position sub-tiles instead
+   * of recomputing it (C2: scan backward -10 %) at 4x the state memory; pair-
+   * kernel shapes only -- mc_scan_fwd_state_interval() resolves a request.
+   * Layout: the default interval keeps (batch, dim, n_states, dstate); the fine
+   * one is position-major, (batch, n_states, dim, dstate). */
+  int32_t state_interval;
 } mc_scan_fwd_params;
 
 typedef struct mc_scan_bwd_params {
@@ -180,13 +192,24 @@ typedef struct mc_scan_bwd_params {
   const void* delta_proj_w;
   int32_t delta_rank;
   int64_t dpx_batch_stride, dpx_token_stride, dpw_dim_stride;
+  /* the interval the forward saved chunk_states with (0 = MC_SCAN_CHUNK) */
+  int32_t state_interval;
 } mc_scan_bwd_params;
 
 /* number of MC_SCAN_CHUNK-long chunks covering seqlen */
 int32_t mc_scan_n_chunks(int32_t seqlen);
 
-/* bytes of fp32 chunk states the forward writes for a training call */
+/* bytes of fp32 chunk states the forward writes for a training call (default interval) */
 size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate);
+
+/* saved states per channel at a given interval (0 = MC_SCAN_CHUNK): ceil(seqlen / interval) */
+int32_t mc_scan_n_states(int32_t seqlen, int32_t state_interval);
+
+/* the interval mc_scan_fwd will save states with for these params: p->state_interval when
+ * the call can honour it (MC_SCAN_STATE_INTERVAL_FINE needs the pair kernel's shapes),
+ * else MC_SCAN_CHUNK.  Size chunk_states with mc_scan_n_states(seqlen, result) and pass
+ * the result to both mc_scan_fwd and mc_scan_bwd. */
+int32_t mc_scan_fwd_state_interval(const mc_scan_fwd_params* p);
 
 /* workspace the forward needs (B/C re-laid out as fp32 [batch][group][seqlen][2*dstate']) */
 size_t mc_scan_fwd_workspace_bytes(int32_t batch, int32_t seqlen, int32_t dstate, int32_t n_groups);

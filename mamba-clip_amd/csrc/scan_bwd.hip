@@ -48,6 +48,7 @@ static_assert(kTC % kTB == 0, "chunk must be whole sub-tiles");
 
 struct BwdArgs {
   int batch, dim, seqlen, dstate, n_groups, n_states, nblk, total_blocks, softplus;
+  int state_ratio;    // saved states per kS-position chunk (kS / the forward's state interval)
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, go_bs, go_ds;
   int64_t du_bs, du_ds, ddt_bs, ddt_ds, dz_bs, dz_ds;  // output strides (seqlen stride 1)
   const void* u; const void* delta; const void* z; const void* dout;
@@ -192,9 +193,13 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
   const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(rb0, span(ds0)), rs1 = make_rsrc(rb1, span(ds1));
   const float* bqsrc = a.bq + (int64_t)bg * L_ * (4 * kP);
   const __amdgpu_buffer_rsrc_t rs_bq = make_rsrc(bqsrc, (uint32_t)L_ * kP * 16u);
-  const uint32_t cs_row = (uint32_t)(a.n_states * a.dstate);   // floats per channel row of chunk states
-  const float* csb = a.chunk_states + ((int64_t)b * a.dim + dbase) * a.n_states * a.dstate;
-  const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(csb, (uint32_t)nrows * cs_row * 4u);
+  // chunk states [b][row][n_states][N]; the fine interval is position-major, [b][n_states][row][N]
+  const bool pm = a.state_ratio != 1;
+  const uint32_t cs_rs = pm ? (uint32_t)a.dstate : (uint32_t)(a.n_states * a.dstate);   // floats per row step
+  const uint32_t cs_ks = pm ? (uint32_t)(a.dim * a.dstate) : (uint32_t)a.dstate;        // floats per state step
+  const float* csb = a.chunk_states + (int64_t)b * a.dim * a.n_states * a.dstate + (int64_t)dbase * cs_rs;
+  const __amdgpu_buffer_rsrc_t rs_cs =
+      make_rsrc(csb, nrows > 0 ? ((uint32_t)(nrows - 1) * cs_rs + (uint32_t)(a.n_states - 1) * cs_ks + a.dstate) * 4u : 0u);
   const __amdgpu_buffer_rsrc_t rs_slab =
       make_rsrc(a.slab_bc + ((int64_t)bg * a.nblk + dblk) * L_ * (2 * kN), (uint32_t)L_ * (2 * kN) * 4u);
 
@@ -261,7 +266,7 @@ __global__ __launch_bounds__(kWG, kMinW) void scan_bwd_kernel(const BwdArgs a) {
       pq[k] = __builtin_bit_cast(f32x4, buf_ld16(rs_bq, o));
     }
     // saved state after chunk c-1 (zero for c == 0): floats [2 kPW wave, 2 kPW (wave+1)) of my row
-    const uint32_t ox = c > 0 ? ((uint32_t)my_r * cs_row + (uint32_t)((c - 1) * a.dstate + 2 * kPW * wave)) * 4u
+    const uint32_t ox = c > 0 ? ((uint32_t)my_r * cs_rs + (uint32_t)(c * a.state_ratio - 1) * cs_ks + (uint32_t)(2 * kPW * wave)) * 4u
                               : 0x80000000u;
 #pragma unroll
     for (int k = 0; k < kPW / 2; ++k) px0[k] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox + 16 * k));
@@ -859,6 +864,13 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
                (int64_t)p->seqlen * 2 * np * 4 < ((int64_t)1 << 31),
            MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit offsets", p->seqlen);
   MC_CHECK(p->chunk_states, MC_ERR_INVALID, "mc_scan_bwd: chunk_states (from the training forward) required");
+  const int S = p->state_interval > 0 ? p->state_interval : kS;
+  MC_CHECK(S == kS || (S == kFineS && p->seqlen % kFineS == 0), MC_ERR_SHAPE,
+           "mc_scan_bwd: state_interval %d: 0 / %d, or %d with seqlen %% %d == 0 (the forward's interval)",
+           p->state_interval, kS, kFineS, kFineS);
+  MC_CHECK((int64_t)kRows * mc_scan_n_states(p->seqlen, S) * p->dstate * 4 < ((int64_t)1 << 31) &&
+               (int64_t)128 * mc_scan_n_states(p->seqlen, S) * 16 * 4 < ((int64_t)1 << 31),   // pair kernel: 128 rows
+           MC_ERR_INVALID, "mc_scan_bwd: seqlen %d too long for 32-bit state offsets", p->seqlen);
   const bool dirs = p->reverse_groups != 0 || p->u_groups != 0;
   if (dirs) {
     MC_CHECK(!p->z && p->u_groups >= 0 && p->u_groups <= p->n_groups && p->n_groups <= 31 &&
@@ -903,7 +915,8 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
 
   BwdArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
-  a.n_states = mc_scan_n_chunks(p->seqlen);
+  a.n_states = mc_scan_n_states(p->seqlen, S);
+  a.state_ratio = kS / S;
   const int H = p->dim / p->n_groups;
   a.nblk = (H + kRows - 1) / kRows;
   a.total_blocks = p->batch * p->n_groups * a.nblk;

@@ -33,22 +33,18 @@
 namespace mc {
 namespace scan {
 
-#ifndef MC_BWD_EXP_NORECOMP
-#define MC_BWD_EXP_NORECOMP 0
-#endif
-#ifndef MC_BWD_EXP_NOY
-#define MC_BWD_EXP_NOY 0
-#endif
 constexpr int kQW = 4;            // waves per workgroup
 constexpr int kQCh = 32;          // channels per wave
 constexpr int kQN = 16;           // dstate
 constexpr int kQP = 4;            // state pairs per lane
 constexpr int kQT = 8;            // positions per sub-tile
 constexpr int kQSub = kS / kQT;   // sub-tiles per chunk
-static_assert(kS == 32 && kQSub == 4, "the pair backward walks the forward's 32-position chunks");
+static_assert(kS == 32 && kQSub == 4 && kFineS == kQT, "the pair backward walks the forward's 32-position chunks "
+              "in 8-position sub-tiles (the fine saved-state interval)");
 
 struct BwdPairArgs {
   int batch, dim, seqlen, n_groups, n_states, nblk, total_blocks;
+  int state_ratio;    // saved states per 32-position chunk: 1 (interval 32) or 4 (interval 8: no recompute)
   int64_t u_bs, u_ds, dt_bs, dt_ds, z_bs, z_ds, go_bs, go_ds;
   int64_t du_bs, du_ds, ddt_bs, ddt_ds, dz_bs, dz_ds;
   int64_t B_bs, B_gs, B_ns, C_bs, C_gs, C_ns;
@@ -146,6 +142,15 @@ __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
   return r + qperm<kQpXor2>(r);   // bit 1
 }
 
+// One global_load_lds_dwordx4: 16 B per lane from gsrc to LDS byte address m0v + 16 * lane (m0v wave-
+// uniform).  asm, so the compiler's waitcnt pass does not drain it early; the caller waits with
+// s_waitcnt vmcnt(0) before reading the slots.  M0 is compiler-reserved: saved and restored here.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0v) : "memory");
+}
+
 template <typename TI>
 __device__ __forceinline__ uint2 buf_ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -160,7 +165,7 @@ __device__ __forceinline__ f32x2 elem2(uint2 w, int i) {   // elements 2i, 2i + 
   return f32x2{elem_f<TI>(q, 2 * i), elem_f<TI>(q, 2 * i + 1)};
 }
 
-template <typename TI, bool kSP, bool kZ, bool kPD>
+template <typename TI, bool kSP, bool kZ, bool kPD, bool kFine>
 __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPairArgs a) {
   using TW = TI;                               // B / C in the activation dtype (x_dbl rows)
   constexpr int kWV = 16 / (int)sizeof(TW);   // B / C elements per 16-B vector
@@ -218,9 +223,13 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   const uint32_t bo_B = (uint32_t)(((lane >> 2) * a.B_ns + 8 * (lane & 3)) * (int64_t)sizeof(TW));
   const uint32_t bo_C = (uint32_t)(((lane >> 2) * a.C_ns + 8 * (lane & 3)) * (int64_t)sizeof(TW));
   // saved chunk states of this wave's rows: [row][n_states][16]
-  const uint32_t cs_row = (uint32_t)(a.n_states * kQN);
-  const __amdgpu_buffer_rsrc_t rs_cs = make_rsrc(a.chunk_states + ((int64_t)b * a.dim + dbase) * cs_row,
-                                                 (uint32_t)nrows * cs_row * 4u);
+  // saved states of this wave's rows: [b][row][n_states][16], or position-major [b][n_states][row][16] at the
+  // fine interval (the forward's 32 rows of one position are then one contiguous 2 KB store)
+  const uint32_t cs_rs = kFine ? (uint32_t)kQN : (uint32_t)(a.n_states * kQN);     // floats per row step
+  const uint32_t cs_ks = kFine ? (uint32_t)(a.dim * kQN) : (uint32_t)kQN;          // floats per state step
+  const __amdgpu_buffer_rsrc_t rs_cs =
+      make_rsrc(a.chunk_states + (int64_t)b * a.dim * a.n_states * kQN + (int64_t)dbase * cs_rs,
+                nrows > 0 ? ((uint32_t)(nrows - 1) * cs_rs + (uint32_t)(a.n_states - 1) * cs_ks + kQN) * 4u : 0u);
 
   // projected delta operands: token-major dpx rows of this batch, the wave's dpw rows
   const __amdgpu_buffer_rsrc_t rs_px =
@@ -254,7 +263,8 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
       pC[k] = buf_ld16(rs_C, (bo_C + lo) + (uint32_t)(k * 16));
     }
     // state after chunk c - 1 (zero for c == 0): floats [8h, 8h + 8) of my row
-    const uint32_t ox = c > 0 ? ((uint32_t)my_r * cs_row + (uint32_t)((c - 1) * kQN + 8 * h)) * 4u : 0x80000000u;
+    const uint32_t ox = c > 0 ? ((uint32_t)my_r * cs_rs + (uint32_t)(c * (kFine ? kS / kQT : 1) - 1) * cs_ks + 8 * h) * 4u
+                              : 0x80000000u;
     px[0] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox));
     px[1] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox + 16));
   };
@@ -310,8 +320,29 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
   auto bquad = [&](int t, int p) __attribute__((always_inline)) -> f32x4 { return bcq[t * (2 * kQP) + h * kQP + p]; };
 
   const int nch = (L_ + kS - 1) / kS;
+  // raw rows walk: with recompute, the pass consumes sub-tiles 0 .. nsub - 2 forward and leaves the
+  // last sub-tile's rows in flight; with fine saved states the main loop starts there directly
+  constexpr bool fine = kFine;
+  // fine states: the entries of sub-tiles 1 .. 3 of chunk c (states after positions 32 c + 8 s + 7)
+  // land in the sub-tile-entry slots by LDS DMA, issued one chunk ahead (after the previous chunk's
+  // sub-tile loop, when the slots are free) and waited for at the chunk start: no VGPRs held
+  typedef __attribute__((address_space(3))) char lds_char_t;
+  const uint32_t xst_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char_t*)(reinterpret_cast<char*>(xst)));
+  const float* cs_lane = a.chunk_states + (int64_t)b * a.dim * a.n_states * kQN + (int64_t)(dbase + my_r) * kQN + 8 * h;
+  auto issue_fine = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < kQSub - 1; ++s) {
+      const float* src = cs_lane + (int64_t)min(c * (kS / kQT) + s, a.n_states - 1) * cs_ks;
+      glds16_asm(src, xst_lds + (uint32_t)(2 * s) * 1024u);
+      glds16_asm(src + 4, xst_lds + (uint32_t)(2 * s + 1) * 1024u);
+    }
+  };
+  if (fine) {
+    issue_fine(nch - 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  }
   load_chunk(nch - 1);
-  load_raw((nch - 1) * kS);
+  load_raw((nch - 1) * kS + (fine ? kQT * (min(kQSub, (L_ - (nch - 1) * kS) / kQT) - 1) : 0));
   int buf = 0;
   for (int c = nch - 1; c >= 0; --c) {
     const int l0 = c * kS;
@@ -371,19 +402,14 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
 #pragma unroll
       for (int p = 0; p < kQP; ++p) x0[p] = f32x2{0.f, 0.f};
     }
+    if (fine) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA of this chunk's entries landed
     load_chunk(c - 1);
     wave_lds_sync();
 
-    // ---- recompute pass: states at the starts of sub-tiles 1 .. nsub - 1 -> LDS
-#if MC_BWD_EXP_NORECOMP   // timing experiment only: states of sub-tile starts read from HBM instead (wrong values)
-    for (int s = 0; s + 1 < nsub; ++s) {
-      const uint32_t ox = ((uint32_t)my_r * cs_row + (uint32_t)(min(c * 4 + s, a.n_states - 1) * kQN + 8 * h)) * 4u;
-      xst[(2 * s) * 64 + lane] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox));
-      xst[(2 * s + 1) * 64 + lane] = __builtin_bit_cast(f32x4, buf_ld16(rs_cs, ox + 16));
-    }
-    if (0)
-#endif
-    {
+    // ---- states at the starts of sub-tiles 1 .. nsub - 1 -> LDS: the forward's fine-interval states
+    // (state_ratio 4: entry of sub-tile s + 1 = the state after position l0 + 8 s + 7), else recomputed
+    if constexpr (fine) {   // already in LDS (issue_fine)
+    } else {
       f32x2 x[kQP];
 #pragma unroll
       for (int p = 0; p < kQP; ++p) x[p] = x0[p];
@@ -417,7 +443,8 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
     for (int s = nsub - 1; s >= 0; --s) {
       const uint2 ru = nu, rz = nz, rg = ng;
       const uint2 rd = kPD ? *reinterpret_cast<const uint2*>(dlt + (my_r * kS + kQT * s + 4 * h) * 2) : nd;
-      load_raw(s > 0 ? l0 + kQT * (s - 1) : l0 - kS);   // next step (next chunk's first sub-tile after s = 0)
+      // next step; after s = 0 the next chunk's first step (full chunk: its last sub-tile when fine)
+      load_raw(s > 0 ? l0 + kQT * (s - 1) : (fine ? l0 - kQT : l0 - kS));
       Sc sc;
       scalars(ru, rd, rz, rg, true, sc);
       // state entering the sub-tile: the chunk start (registers) or the recompute pass's (LDS)
@@ -482,9 +509,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
             if (t > 0) qn = bquad(kQT * s + t - 1, p);
             lam = (t & 1) ? pk_fma_bcast<1>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha)
                           : pk_fma_bcast<0>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha);
-#if !MC_BWD_EXP_NOY
             if (hasZ) Y2[t] = q.hi * xs[t] + Y2[t];
-#endif
             S2[t] = lam * q.lo + S2[t];
             red[t] = (t & 1) ? pk_mul_bcast<1>(lam, sc.dtu[t >> 1]) : pk_mul_bcast<0>(lam, sc.dtu[t >> 1]);
             ha = lam * as[t];
@@ -515,7 +540,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
       }
       float fY[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) fY[e] = MC_BWD_EXP_NOY ? 0.f : pair_finish(Y2[e], Y2[4 + e], h);
+      for (int e = 0; e < 4; ++e) fY[e] = pair_finish(Y2[e], Y2[4 + e], h);
       float o_du[4], o_dd[4], o_dz[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -553,6 +578,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
         buf_st8(rs_dz, ((ro_dz + e0) * 2u) | st_mask, make_uint2(cvt_pk2<TI>(o_dz[0], o_dz[1]), cvt_pk2<TI>(o_dz[2], o_dz[3])));
     }
 
+    if (fine && c > 0) issue_fine(c - 1);   // the slots are free: this chunk's sub-tiles are done
     // ---- dB / dC of the chunk: sum over the workgroup's waves (fixed order) -> slab
     lds_barrier();
     {
@@ -615,17 +641,24 @@ bool bwd_pair_ok(const mc_scan_bwd_params* p) {
          rows(p->dz, p->dz_batch_stride, p->dz_dim_stride) &&
          bc(p->B, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride) &&
          bc(p->C, p->C_batch_stride, p->C_group_stride, p->C_dstate_stride) &&
-         (int64_t)kQCh * kQW * mc_scan_n_chunks(p->seqlen) * kQN * 4 < ((int64_t)1 << 31);
+         (int64_t)kQCh * kQW * mc_scan_n_states(p->seqlen, p->state_interval) * kQN * 4 < ((int64_t)1 << 31);
 }
 
 template <typename TI, bool kPD>
 static void launch_pair_pd(const BwdPairArgs& a, bool sp, bool zy, hipStream_t s) {
   const size_t lds = bwd_pair_lds_bytes(kPD);
   const dim3 grid(a.total_blocks), block(64 * kQW);
-  if (sp && zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, true, kPD>), grid, block, lds, s, a);
-  else if (sp) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, false, kPD>), grid, block, lds, s, a);
-  else if (zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, true, kPD>), grid, block, lds, s, a);
-  else hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, false, kPD>), grid, block, lds, s, a);
+  if (a.state_ratio != 1) {
+    if (sp && zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, true, kPD, true>), grid, block, lds, s, a);
+    else if (sp) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, false, kPD, true>), grid, block, lds, s, a);
+    else if (zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, true, kPD, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, false, kPD, true>), grid, block, lds, s, a);
+    return;
+  }
+  if (sp && zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, true, kPD, false>), grid, block, lds, s, a);
+  else if (sp) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, true, false, kPD, false>), grid, block, lds, s, a);
+  else if (zy) hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, true, kPD, false>), grid, block, lds, s, a);
+  else hipLaunchKernelGGL((scan_bwd_pair_kernel<TI, false, false, kPD, false>), grid, block, lds, s, a);
 }
 template <typename TI>
 static void launch_pair_t(const BwdPairArgs& a, bool sp, bool zy, hipStream_t s) {
@@ -637,7 +670,8 @@ void launch_bwd_pair(const mc_scan_bwd_params* p, float* slab_bc, float* slab_a,
                      int nblk, hipStream_t s) {
   BwdPairArgs a;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.n_groups = p->n_groups;
-  a.n_states = mc_scan_n_chunks(p->seqlen);
+  a.n_states = mc_scan_n_states(p->seqlen, p->state_interval);
+  a.state_ratio = p->state_interval == kFineS ? kS / kFineS : 1;
   a.nblk = nblk;
   a.total_blocks = p->batch * p->n_groups * nblk;
   a.u_bs = p->u_batch_stride; a.u_ds = p->u_dim_stride;

@@ -9,6 +9,7 @@ namespace scan {
 
 constexpr int kT = 32;             // sequence positions per forward tile
 constexpr int kS = MC_SCAN_CHUNK;  // positions per saved chunk state (32)
+constexpr int kFineS = MC_SCAN_STATE_INTERVAL_FINE;   // the fine saved-state interval (8)
 constexpr int kRows = 64;          // channels per workgroup: one wave
 
 // B/C as the recurrence consumes them: fp32, position-major, [b][g][l][2*kNp]
@@ -262,6 +263,7 @@ struct FwdArgs {
   // B / C rows as given (the pair kernel reads them directly; the others read the relaid bct)
   const void* B; const void* C;
   int64_t B_bs, B_gs, B_ns, C_bs, C_gs, C_ns;
+  int state_interval;                // positions per saved state (pair kernel: 8 or 32; others 32)
 };
 
 int validate_common(int batch, int dim, int seqlen, int dstate, int n_groups, int itype, int wtype, const char* who);

@@ -735,6 +735,11 @@ using namespace mc::scan;
 
 extern "C" int32_t mc_scan_n_chunks(int32_t seqlen) { return seqlen <= 0 ? 0 : (seqlen + kS - 1) / kS; }
 
+extern "C" int32_t mc_scan_n_states(int32_t seqlen, int32_t state_interval) {
+  const int S = state_interval > 0 ? state_interval : kS;
+  return seqlen <= 0 ? 0 : (seqlen + S - 1) / S;
+}
+
 extern "C" size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate) {
   return (size_t)batch * dim * mc_scan_n_chunks(seqlen) * dstate * sizeof(float);
 }
@@ -742,6 +747,8 @@ extern "C" size_t mc_scan_chunk_states_bytes(int32_t batch, int32_t dim, int32_t
 extern "C" size_t mc_scan_fwd_workspace_bytes(int32_t batch, int32_t seqlen, int32_t dstate, int32_t n_groups) {
   return bct_bytes(batch, seqlen, dstate, n_groups);
 }
+
+static bool fill_fwd_args(const mc_scan_fwd_params* p, FwdArgs& a, bool& aligned);
 
 extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_scan_fwd: null params");
@@ -784,6 +791,47 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
              p->n_groups);
   }
   FwdArgs a;
+  bool aligned = false;
+  const bool pair = fill_fwd_args(p, a, aligned);
+  const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
+  (void)dirs;
+  MC_CHECK(p->state_interval == 0 || p->state_interval == kS || (p->state_interval == kFineS && pair), MC_ERR_SHAPE,
+           "mc_scan_fwd: state_interval %d: 0 / %d, or %d on the pair kernel's shapes (mc_scan_fwd_state_interval)",
+           p->state_interval, kS, kFineS);
+  // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
+  // forward 0.166 vs 0.183 ms per layer).  It reads B / C rows itself: no relayout pre-pass.
+  if (pair) return launch_fwd_pair(a, p->itype, s);
+  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
+                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
+                             p->seqlen, p->dstate, dirs ? p->reverse_groups : 0,
+                             reinterpret_cast<float*>(p->workspace), s);
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
+  if (dirs) {   // per-group addressing lives in the LDS-staged kernel (vector modes: seqlen % VI == 0)
+    MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta and grouped directions do not combine");
+    const bool al = aligned && p->seqlen % (16 / ib) == 0;
+    if (p->itype == MC_DTYPE_F32) return launch_fwd_dirs<float>(a, al, s);
+    if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
+    return launch_fwd_dirs<f16_t>(a, al, s);
+  }
+  MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta needs the pair kernel's shapes (16-bit rows, "
+           "dstate 16, seqlen %% 8 == 0, 16-B aligned rows, no grouped directions)");
+  if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
+  if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
+  return launch_fwd_t<f16_t>(a, aligned, s);
+}
+
+extern "C" int32_t mc_scan_fwd_state_interval(const mc_scan_fwd_params* p) {
+  if (!p || p->state_interval != kFineS) return kS;
+  FwdArgs a;
+  bool aligned = false;
+  return fill_fwd_args(p, a, aligned) ? kFineS : kS;
+}
+
+// FwdArgs from validated params; returns whether the pair kernel takes the call.  a.state_interval is
+// the fine interval only when requested and the pair kernel runs (the others save every kS).
+static bool fill_fwd_args(const mc_scan_fwd_params* p, FwdArgs& a, bool& aligned) {
+  const bool proj = p->delta_proj_w != nullptr;
+  const bool dirs = p->reverse_groups != 0 || p->u_groups != 0;
   a.batch = p->batch; a.dim = p->dim; a.seqlen = p->seqlen; a.dstate = p->dstate; a.n_groups = p->n_groups;
   a.n_chunks = (p->seqlen + kT - 1) / kT;
   a.n_states = mc_scan_n_chunks(p->seqlen);
@@ -808,29 +856,13 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   a.C_bs = p->C_batch_stride; a.C_gs = p->C_group_stride; a.C_ns = p->C_dstate_stride;
 
   const int ib = p->itype == MC_DTYPE_F32 ? 4 : 2;
-  const bool aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
-                       vec_ok(proj ? p->delta_out : p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
-                       vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
-                       vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
-                       vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
-  // 16-bit rows, N = 16: state-split lane pairs (scan_fwd_pair.hip; C4 2.78 vs 3.22 ms, C2 training
-  // forward 0.166 vs 0.183 ms per layer).  It reads B / C rows itself: no relayout pre-pass.
-  if (!dirs && fwd_pair_ok(a, aligned, ib, p->itype, p->wtype)) return launch_fwd_pair(a, p->itype, s);
-  hipError_t e = relayout_bc(p->wtype, p->B, p->C, p->B_batch_stride, p->B_group_stride, p->B_dstate_stride,
-                             p->C_batch_stride, p->C_group_stride, p->C_dstate_stride, p->batch, p->n_groups,
-                             p->seqlen, p->dstate, dirs ? p->reverse_groups : 0,
-                             reinterpret_cast<float*>(p->workspace), s);
-  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: B/C relayout launch failed: %s", hipGetErrorString(e));
-  if (dirs) {   // per-group addressing lives in the LDS-staged kernel (vector modes: seqlen % VI == 0)
-    MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta and grouped directions do not combine");
-    const bool al = aligned && p->seqlen % (16 / ib) == 0;
-    if (p->itype == MC_DTYPE_F32) return launch_fwd_dirs<float>(a, al, s);
-    if (p->itype == MC_DTYPE_BF16) return launch_fwd_dirs<bf16_t>(a, al, s);
-    return launch_fwd_dirs<f16_t>(a, al, s);
-  }
-  MC_CHECK(!proj, MC_ERR_SHAPE, "mc_scan_fwd: projected delta needs the pair kernel's shapes (16-bit rows, "
-           "dstate 16, seqlen %% 8 == 0, 16-B aligned rows, no grouped directions)");
-  if (p->itype == MC_DTYPE_F32) return launch_fwd_t<float>(a, aligned, s);
-  if (p->itype == MC_DTYPE_BF16) return launch_fwd_t<bf16_t>(a, aligned, s);
-  return launch_fwd_t<f16_t>(a, aligned, s);
+  aligned = vec_ok(p->u, p->u_batch_stride, p->u_dim_stride, 0, ib) &&
+            vec_ok(proj ? p->delta_out : p->delta, p->delta_batch_stride, p->delta_dim_stride, 0, ib) &&
+            vec_ok(p->z, p->z_batch_stride, p->z_dim_stride, 0, ib) &&
+            vec_ok(p->out, p->out_batch_stride, p->out_dim_stride, 0, ib) &&
+            vec_ok(a.out_y, a.y_bs, a.y_ds, 0, ib);
+  const bool pair = !dirs && fwd_pair_ok(a, aligned, ib, p->itype, p->wtype);
+  a.state_interval = (pair && p->state_interval == kFineS) ? kFineS : kS;
+  a.n_states = mc_scan_n_states(p->seqlen, a.state_interval);
+  return pair;
 }

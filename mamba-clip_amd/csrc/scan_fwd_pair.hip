@@ -33,6 +33,9 @@ namespace mc {
 namespace scan {
 
 constexpr int kPCh = 32;   // channels per wave
+#ifndef MC_FWD_FINE_NT
+#define MC_FWD_FINE_NT 0   // fine saved states with non-temporal stores (A/B lever)
+#endif
 constexpr int kPN = 16;    // dstate
 constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
@@ -309,11 +312,25 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           y2 = c1v.hi * x[3] + y2;
           yv[e] = y2.x + y2.y;
         }
+        if (a.state_interval == kFineS && ((t0 + kPG) % kFineS) == 0 && l0 + t0 + kPG <= L_ && a.chunk_states && my_ok) {
+          // fine interval: the state after position l0 + t0 + kPG - 1 (L % 8 == 0: the last one is L - 1)
+          // position-major [b][n_states][dim][16]: the wave's 32 rows of one position are 2 KB contiguous
+          float4* cs = reinterpret_cast<float4*>(
+              a.chunk_states + (((int64_t)b * a.n_states + (l0 + t0 + kPG) / kFineS - 1) * a.dim + dbase + ch) * kPN +
+              kPH * h);
+#if MC_FWD_FINE_NT
+          __builtin_nontemporal_store(f32x4{x[0].x, x[0].y, x[1].x, x[1].y}, reinterpret_cast<f32x4*>(cs));
+          __builtin_nontemporal_store(f32x4{x[2].x, x[2].y, x[3].x, x[3].y}, reinterpret_cast<f32x4*>(cs) + 1);
+#else
+          cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
+          cs[1] = make_float4(x[2].x, x[2].y, x[3].x, x[3].y);
+#endif
+        }
         // partial y over the {dt, du} bytes both lanes of the pair have consumed
         *reinterpret_cast<float4*>(const_cast<char*>(row) + t0 * 8 + 16 * h) = make_float4(yv[0], yv[1], yv[2], yv[3]);
       }
     }
-    if (a.chunk_states && my_ok && c0 < a.n_states) {   // state after position l0 + kT - 1 (kS == kT)
+    if (a.state_interval == kS && a.chunk_states && my_ok && c0 < a.n_states) {   // state after l0 + kT - 1 (kS == kT)
       float4* cs = reinterpret_cast<float4*>(a.chunk_states +
                                              (((int64_t)b * a.dim + dbase + ch) * a.n_states + c0) * kPN + kPH * h);
       cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("MAMBA_CLIP_AMD_LIB") or os.path.join(_HERE, "libmamba
 MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3, MC_DTYPE_U8 = 0, 1, 2, 3, 4
 MC_LAYOUT_NCHW, MC_LAYOUT_NHWC = 0, 1
 MC_SCAN_CHUNK = 32
+MC_SCAN_STATE_INTERVAL_FINE = 8
 MC_SCAN_MAX_DSTATE = 32
 MC_CAST_CHUNK = 16384
 
@@ -39,7 +40,7 @@ class ScanFwdParams(ctypes.Structure):
         ("reverse_groups", c_i32), ("u_groups", c_i32),
         ("delta_proj_x", c_vp), ("delta_proj_w", c_vp), ("delta_rank", c_i32),
         ("dpx_batch_stride", c_i64), ("dpx_token_stride", c_i64), ("dpw_dim_stride", c_i64),
-        ("delta_out", c_vp),
+        ("delta_out", c_vp), ("state_interval", c_i32),
     ]
 
 
@@ -66,6 +67,7 @@ class ScanBwdParams(ctypes.Structure):
         ("reverse_groups", c_i32), ("u_groups", c_i32),
         ("delta_proj_x", c_vp), ("delta_proj_w", c_vp), ("delta_rank", c_i32),
         ("dpx_batch_stride", c_i64), ("dpx_token_stride", c_i64), ("dpw_dim_stride", c_i64),
+        ("state_interval", c_i32),
     ]
 
 
@@ -175,6 +177,8 @@ SYMBOLS = {
     "mc_last_error": (ctypes.c_char_p, []),
     "mc_version": (ctypes.c_char_p, []),
     "mc_scan_n_chunks": (c_i32, [c_i32]),
+    "mc_scan_n_states": (c_i32, [c_i32, c_i32]),
+    "mc_scan_fwd_state_interval": (c_i32, [ctypes.POINTER(ScanFwdParams)]),
     "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),

@@ -11,6 +11,8 @@ fp32 chunk states (one per MC_SCAN_CHUNK positions); the backward runs
 ``mc_scan_bwd`` from them.  Both launch on the current HIP stream and never
 synchronise.  There is no CPU / eager fallback.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -56,6 +58,25 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
         raise RuntimeError("selective_scan_fn: dim must be divisible by n_groups")
 
 
+def fine_states_max_bytes():
+    """Largest saved-state buffer (bytes, one scan call) kept at the fine interval: 4x the default
+    interval's memory buys the backward's recompute pass (C2 layer: 252 MB; a C4 layer at L 4096 would
+    be 6.4 GB and keeps the default).  MAMBA_CLIP_AMD_FINE_STATES_MB overrides (0 = never)."""
+    return int(float(os.environ.get("MAMBA_CLIP_AMD_FINE_STATES_MB", "1024")) * (1 << 20))
+
+
+def states_interval(L, dim, states):
+    """The interval a forward saved `states` with: default (B, dim, ceil(L / 32), N), or fine and
+    position-major (B, ceil(L / 8), dim, N)."""
+    fine = _lib.MC_SCAN_STATE_INTERVAL_FINE
+    n_fine, n_def = -(-L // fine), -(-L // _lib.MC_SCAN_CHUNK)
+    if states.shape[1] == dim and states.shape[2] == n_def:
+        return 0
+    if states.shape[1] == n_fine and states.shape[2] == dim:
+        return fine
+    raise RuntimeError(f"scan states of shape {tuple(states.shape)} match neither interval (L {L}, dim {dim})")
+
+
 def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, want_last, want_y=False,
              dirs=None, proj=None):
     """Run mc_scan_fwd.  Returns (out, chunk_states or None, last_state or None[, out_y]).
@@ -79,9 +100,6 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     G = B.shape[1]
     # same (dense) layout as u: channel-major callers stay channel-major
     out = torch.empty_like(u) if dirs is None else torch.empty_like(delta)
-    nch = _lib.MC_SCAN_CHUNK and lib.mc_scan_n_chunks(L)
-    states = (torch.empty(batch, dim, nch, dstate, device=u.device, dtype=torch.float32)
-              if want_states else None)
     last = (torch.empty(batch, dim, dstate, device=u.device, dtype=torch.float32)
             if want_last and not want_states else None)
     p = _lib.ScanFwdParams()
@@ -98,7 +116,7 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     p.C_batch_stride, p.C_group_stride, p.C_dstate_stride = C.stride(0), C.stride(1), C.stride(2)
     p.u, p.delta, p.A, p.B, p.C = u.data_ptr(), _lib.ptr(delta), A.data_ptr(), B.data_ptr(), C.data_ptr()
     p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
-    p.out, p.chunk_states, p.last_state = out.data_ptr(), _lib.ptr(states), _lib.ptr(last)
+    p.out, p.last_state = out.data_ptr(), _lib.ptr(last)
     if proj is not None:
         dpx, dpw, delta_out = proj
         p.delta_proj_x, p.delta_proj_w, p.delta_rank = dpx.data_ptr(), dpw.data_ptr(), dpw.shape[1]
@@ -114,9 +132,24 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     out_y = torch.empty_like(u) if (want_y and z is not None) else None
     if out_y is not None:
         p.out_y, p.out_y_batch_stride, p.out_y_dim_stride = out_y.data_ptr(), out_y.stride(0), out_y.stride(1)
+    states, nch = None, 0
+    if want_states:
+        # the fine saved-state interval where the pair kernel runs and the states fit the budget:
+        # the backward then reads each sub-tile's entry state instead of recomputing it
+        fine = _lib.MC_SCAN_STATE_INTERVAL_FINE
+        if batch * dim * lib.mc_scan_n_states(L, fine) * dstate * 4 <= fine_states_max_bytes():
+            p.state_interval = fine
+            p.state_interval = lib.mc_scan_fwd_state_interval(p)
+        nch = lib.mc_scan_n_states(L, p.state_interval)
+        shape = (batch, nch, dim, dstate) if p.state_interval == fine else (batch, dim, nch, dstate)
+        states = torch.empty(shape, device=u.device, dtype=torch.float32)
+        p.chunk_states = states.data_ptr()
     _lib.check(lib.mc_scan_fwd(p, _lib.stream_handle(u.device)), "mc_scan_fwd")
     if want_last and states is not None:
-        last = states[:, :, -1, :] if nch > 0 else torch.zeros(batch, dim, dstate, device=u.device)
+        if nch == 0:
+            last = torch.zeros(batch, dim, dstate, device=u.device)
+        else:
+            last = states[:, -1] if p.state_interval == _lib.MC_SCAN_STATE_INTERVAL_FINE else states[:, :, -1, :]
     if want_y:
         return out, states, last, out_y
     return out, states, last
@@ -161,6 +194,7 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
                                    B.data_ptr(), C.data_ptr())
     p.D, p.z, p.delta_bias = _lib.ptr(D), _lib.ptr(z), _lib.ptr(delta_bias)
     p.dout, p.chunk_states = dout.data_ptr(), states.data_ptr()
+    p.state_interval = states_interval(L, dim, states)
     if proj is not None:
         dpx, dpw = proj
         p.delta_proj_x, p.delta_proj_w, p.delta_rank = dpx.data_ptr(), dpw.data_ptr(), dpw.shape[1]

@@ -396,3 +396,57 @@ def test_scan_projected_delta_rejects_bad_shapes():
     with pytest.raises(RuntimeError, match="pair kernel"):
         scan_fwd(u60, None, A, Bm[..., :60].contiguous(), Bm[..., :60].contiguous(), None, None, None, True, False,
                  False, proj=(dpx[:, :60], W, None))
+
+
+# ----------------------------------------------------------------- saved-state interval
+@pytest.mark.parametrize("case", [(2, 256, 64, torch.bfloat16, True), (2, 96, 1000, torch.bfloat16, True),
+                                  (1, 80, 544, torch.float16, False), (3, 128, 8, torch.bfloat16, True),
+                                  (2, 192, 80, torch.bfloat16, True)])
+def test_scan_bwd_fine_state_interval(case, monkeypatch):
+    """The training forward saves the state every 8 positions where the pair kernel runs (the backward
+    reads its sub-tiles' entry states instead of recomputing them, include/mc_scan.h state_interval):
+    gradients vs the fp64 oracle at both intervals, and the two intervals within fp32 rounding of
+    each other (the forward's and the backward's recurrences round the same terms)."""
+    from mamba_clip_amd import selective_scan_interface as ssi
+    batch, dim, L, it, z = case
+    x = _rand_case(batch, dim, L, 16, 1, it, it, z=z, seed=L + dim)
+    dout = torch.randn(batch, dim, L, generator=torch.Generator().manual_seed(8))
+    grads = {}
+    for mb in ("1024", "0"):
+        monkeypatch.setenv("MAMBA_CLIP_AMD_FINE_STATES_MB", mb)
+        dx = {k: (v.to(DEV) if v is not None else None) for k, v in x.items()}
+        out, states, _ = ssi.scan_fwd(dx["u"], dx["delta"], dx["A"], dx["B"], dx["C"], dx["D"], dx["z"],
+                                      dx["delta_bias"], True, True, False)
+        fine = mb != "0"
+        assert states.shape == ((batch, -(-L // 8), dim, 16) if fine else (batch, dim, -(-L // 32), 16))
+        if fine and L > 8:
+            assert ssi.states_interval(L, dim, states) == 8
+        _check_backward(x, True, dout, it)
+        g = ssi.scan_bwd(dx["u"], dx["delta"], dx["A"], dx["B"], dx["C"], dx["D"], dx["z"], dx["delta_bias"],
+                         True, dout.to(DEV).to(it), states)
+        grads[mb] = [t.float() if t is not None else None for t in g]
+    for a, b in zip(grads["1024"], grads["0"]):
+        if a is not None:
+            assert float((a - b).abs().max()) <= 2e-2 * float(b.abs().max()) + 1e-6
+
+
+def test_scan_bwd_generic_kernel_reads_fine_states():
+    """Fine states from the pair forward, backward on the element-wise kernel (dout rows not 16-B
+    aligned): it picks every fourth saved state.  Gradients vs the fp64 oracle."""
+    from mamba_clip_amd import selective_scan_interface as ssi
+    batch, dim, L = 2, 128, 96
+    x = _rand_case(batch, dim, L, 16, 1, torch.bfloat16, torch.bfloat16, z=True, seed=21)
+    dx = {k: (v.to(DEV) if v is not None else None) for k, v in x.items()}
+    out, states, _ = ssi.scan_fwd(dx["u"], dx["delta"], dx["A"], dx["B"], dx["C"], dx["D"], dx["z"],
+                                  dx["delta_bias"], True, True, False)
+    assert states.shape == (batch, L // 8, dim, 16)
+    dout = torch.randn(batch, dim, L, generator=torch.Generator().manual_seed(2)).to(torch.bfloat16)
+    big = torch.zeros(batch, dim, L + 1, dtype=torch.bfloat16, device=DEV)
+    big[:, :, 1:] = dout.to(DEV)
+    dview = big[:, :, 1:]                      # rows start 2 B past a 16-B boundary
+    du, ddelta, dA, dB, dC, dD, dz, dbias = ssi.scan_bwd(dx["u"], dx["delta"], dx["A"], dx["B"], dx["C"], dx["D"],
+                                                         dx["z"], dx["delta_bias"], True, dview, states)
+    ref = selective_scan_ref_grads(**x, delta_softplus=True, dout=dout.double(), compute_dtype=torch.float64)
+    got = dict(u=du, delta=ddelta, A=dA, B=dB, C=dC, D=dD, z=dz, delta_bias=dbias)
+    for k, g in ref.items():
+        assert_grad_close(got[k], g, torch.bfloat16 if k in ("u", "delta", "z", "B", "C") else torch.float32, k)
