@@ -72,7 +72,7 @@ def test_c1_shape_matches_cpu_restatement():
         ref_loss = oracle_clip_loss(**ref)["contrastive_loss"]
         ref_loss.backward()
     assert _rel(out["text_features"], ref["text_features"]) < 1e-4
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    assert abs(float(loss.detach()) - float(ref_loss.detach())) <= 1e-5 * max(1.0, abs(float(ref_loss.detach())))
     rp = dict(cpu.named_parameters())
     for n, p in gpu.named_parameters():
         if p.grad is not None:
