@@ -154,6 +154,44 @@ typedef struct {
 } mc_cast_chunk;
 int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, void* dst_base, int32_t dst_dtype, void* stream);
 
+/* ---- Mamba mixer projections (mixer_proj.hip): x_proj and dt_proj around the scan, fused.
+ * Reference: the mixer's x_dbl = x_proj(x), delta = dt_proj.weight @ dt_raw (upstream
+ * mamba_simple.Mamba; SS2D's analogue model.py:519-528, 630-647).  Channel-major activations
+ * (dim, tokens), tokens contiguous; all 16-bit (dtype bf16 / f16), weights contiguous.
+ *   forward:  x_dbl (P, T) = w_x (P, D) . x (D, T), rounded to dtype;
+ *             delta (D, T) = w_dt (D, R) . x_dbl[0:R], rounded (no bias: the scan adds it)
+ *   backward: d_x_dbl (P, T) = [w_dt^T . g_delta + g_x_dbl[0:R] ; g_x_dbl[R:P]], rounded;
+ *             dx (D, T) = w_x^T . d_x_dbl + du (du nullable), rounded once
+ * The weight gradients are left to the caller (they are reductions over T).
+ * Requirements: dim % 64 == 0, tokens % 8 == 0, rank % 16 == 0 in [16, 96], proj_rows = rank + 32
+ * (dstate 16: every reference config); 16-B aligned rows (strides % 8 elements; du 8-B), w_dt
+ * 8-B aligned. */
+typedef struct mc_mixer_proj_params {
+  int32_t dim, tokens, rank, proj_rows, dtype;
+  int64_t x_ld, x_dbl_ld, delta_ld;      /* row strides (elements) */
+  const void* x;                          /* (dim, tokens) */
+  const void* w_x;                        /* (proj_rows, dim): x_proj.weight */
+  const void* w_dt;                       /* (dim, rank): dt_proj.weight */
+  void* x_dbl;                            /* (proj_rows, tokens) out */
+  void* delta;                            /* (dim, tokens) out */
+} mc_mixer_proj_params;
+
+int mc_mixer_proj_fwd(const mc_mixer_proj_params* p, void* stream);
+
+typedef struct mc_mixer_proj_bwd_params {
+  int32_t dim, tokens, rank, proj_rows, dtype;
+  int64_t g_delta_ld, g_x_dbl_ld, du_ld, d_x_dbl_ld, dx_ld;
+  const void* g_delta;                    /* (dim, tokens): gradient of delta */
+  const void* g_x_dbl;                    /* nullable (proj_rows, tokens): gradient of x_dbl (dB / dC rows) */
+  const void* w_x;
+  const void* w_dt;
+  const void* du;                         /* nullable (dim, tokens): the other consumer's gradient of x */
+  void* d_x_dbl;                          /* (proj_rows, tokens) out */
+  void* dx;                               /* (dim, tokens) out */
+} mc_mixer_proj_bwd_params;
+
+int mc_mixer_proj_bwd(const mc_mixer_proj_bwd_params* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,25 @@ class ScanBwdParams(ctypes.Structure):
     ]
 
 
+class MixerProjParams(ctypes.Structure):
+    """Mirror of ``mc_mixer_proj_params`` (include/mc_ops.h)."""
+    _fields_ = [
+        ("dim", c_i32), ("tokens", c_i32), ("rank", c_i32), ("proj_rows", c_i32), ("dtype", c_i32),
+        ("x_ld", c_i64), ("x_dbl_ld", c_i64), ("delta_ld", c_i64),
+        ("x", c_vp), ("w_x", c_vp), ("w_dt", c_vp), ("x_dbl", c_vp), ("delta", c_vp),
+    ]
+
+
+class MixerProjBwdParams(ctypes.Structure):
+    """Mirror of ``mc_mixer_proj_bwd_params`` (include/mc_ops.h)."""
+    _fields_ = [
+        ("dim", c_i32), ("tokens", c_i32), ("rank", c_i32), ("proj_rows", c_i32), ("dtype", c_i32),
+        ("g_delta_ld", c_i64), ("g_x_dbl_ld", c_i64), ("du_ld", c_i64), ("d_x_dbl_ld", c_i64), ("dx_ld", c_i64),
+        ("g_delta", c_vp), ("g_x_dbl", c_vp), ("w_x", c_vp), ("w_dt", c_vp), ("du", c_vp),
+        ("d_x_dbl", c_vp), ("dx", c_vp),
+    ]
+
+
 class GemmNTParams(ctypes.Structure):
     """Mirror of ``mc_gemm_nt_params`` (include/mc_contrastive.h)."""
     _fields_ = [
@@ -222,6 +241,8 @@ SYMBOLS = {
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),
+    "mc_mixer_proj_fwd": (ctypes.c_int, [ctypes.POINTER(MixerProjParams), c_vp]),
+    "mc_mixer_proj_bwd": (ctypes.c_int, [ctypes.POINTER(MixerProjBwdParams), c_vp]),
     "mc_patch_embed_input": (ctypes.c_int, [ctypes.POINTER(PatchInputParams), c_vp]),
     "mc_ss2d_conv_stack_fwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvParams), c_vp]),
     "mc_ss2d_conv_stack_bwd": (ctypes.c_int, [ctypes.POINTER(SS2DConvBwdParams), c_vp]),

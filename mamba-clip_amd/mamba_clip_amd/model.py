@@ -32,7 +32,7 @@ import torch.utils.checkpoint
 
 from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
-                  fc1_gelu, linear_sk, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
+                  fc1_gelu, linear_sk, mixer_proj, mixer_proj_ok, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
                   ss2d_conv_stack, ss2d_merge_ln_gate, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
@@ -87,6 +87,8 @@ class MambaMixer(nn.Module):
         # saves (C2 step 88.4 vs 86.5 ms on one box, profiles/r03/c2_ab_fuse_dt_proj.txt)
         self.fuse_dt_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_DT_PROJ", "0") == "1"   # A/B toggle
         self.du_handoff = True   # scan du -> x_proj's dX epilogue (ops.GradHandoff)
+        # x_proj + dt_proj as one HIP pass each way (ops.MixerProjFn); A/B toggle
+        self.fuse_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_MIXER_PROJ", "1") != "0"
 
     def forward(self, hidden, A=None):  # (B, L, d_model) contiguous; A: -exp(A_log) when the tower formed it
         Bsz, L, dm = hidden.shape
@@ -115,6 +117,15 @@ class MambaMixer(nn.Module):
             Cm = BC[N:].view(N, Bsz, L).transpose(0, 1)
             y = ProjectedScanFn.apply(x, dt_raw, self.dt_proj.weight, A, Bm, Cm, self.D.float(), z,
                                       self.dt_proj.bias.float(), True, dz)
+        elif self.fuse_proj and mixer_proj_ok(x_cm, R, N):
+            # x_proj and dt_proj in one pass over x (and one backward pass over ddelta that also adds
+            # the scan's du into dx: ops.GradHandoff)
+            hand = GradHandoff() if (self.du_handoff and x.requires_grad) else None
+            x_dbl, delta = mixer_proj(x_cm, self.x_proj.weight, self.dt_proj.weight, hand)
+            Bm = x_dbl[R:R + N].view(N, Bsz, L).transpose(0, 1)                # (B, N, L)
+            Cm = x_dbl[R + N:].view(N, Bsz, L).transpose(0, 1)
+            delta = delta.view(di, Bsz, L).transpose(0, 1)
+            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz, hand)
         else:
             # x's gradient: the scan's du is handed to x_proj's backward, which adds its dX in the
             # GEMM epilogue (ops.GradHandoff) instead of autograd summing the two producers

@@ -889,6 +889,79 @@ def wleft_mm(weight, X, handoff=None):
     return WeightLeftMM.apply(weight, X, handoff)
 
 
+def mixer_proj_ok(x_cm, rank, dstate):
+    """Shapes mc_mixer_proj_* take: 16-bit (D, T) rows with unit token stride, D % 64, T % 8, rank % 16
+    in [16, 96], dstate 16 (every reference config)."""
+    dt = _compute_dtype(x_cm)
+    D, T = x_cm.shape
+    return (x_cm.is_cuda and dt in (torch.bfloat16, torch.float16) and x_cm.stride(1) == 1 and D % 64 == 0
+            and T % 8 == 0 and T > 0 and rank % 16 == 0 and 16 <= rank <= 96 and dstate == 16
+            and x_cm.stride(0) % 8 == 0 and x_cm.data_ptr() % 16 == 0)
+
+
+class MixerProjFn(torch.autograd.Function):
+    """x_dbl = x_proj(x), delta = dt_proj.weight @ x_dbl[:R] for the Mamba mixer's channel-major
+    activations (D, T), in one HIP pass (mc_mixer_proj_fwd); backward: d_x_dbl and dx = x_proj^T d_x_dbl
+    + du (the scan's gradient, handed over by ops.GradHandoff) in one pass (mc_mixer_proj_bwd), the two
+    weight gradients as split-K GEMMs (ops.wgrad).  Same roundings as the library-GEMM chain:
+    x_dbl, delta, d_dtraw and dx stored once in the activation dtype."""
+
+    @staticmethod
+    def forward(ctx, x, w_x, w_dt, handoff):
+        dt = _compute_dtype(x)
+        lib = _lib.load()
+        xc = x if x.dtype == dt else x.to(dt)
+        wx, wdt = _wcast(w_x, dt).contiguous(), _wcast(w_dt, dt).contiguous()
+        D, T = xc.shape
+        P, R = wx.shape[0], wdt.shape[1]
+        xd = torch.empty(P, T, device=xc.device, dtype=dt)
+        delta = torch.empty(D, T, device=xc.device, dtype=dt)
+        p = _lib.MixerProjParams()
+        p.dim, p.tokens, p.rank, p.proj_rows, p.dtype = D, T, R, P, _lib.dtype_code(dt)
+        p.x_ld, p.x_dbl_ld, p.delta_ld = xc.stride(0), T, T
+        p.x, p.w_x, p.w_dt, p.x_dbl, p.delta = xc.data_ptr(), wx.data_ptr(), wdt.data_ptr(), xd.data_ptr(), delta.data_ptr()
+        _lib.check(lib.mc_mixer_proj_fwd(ctypes.byref(p), _lib.stream_handle(xc.device)), "mc_mixer_proj_fwd")
+        ctx.save_for_backward(xc, wx, wdt, xd)
+        ctx.handoff = handoff
+        return xd, delta
+
+    @staticmethod
+    def backward(ctx, g_xd, g_delta):
+        xc, wx, wdt, xd = ctx.saved_tensors
+        lib = _lib.load()
+        D, T = xc.shape
+        P, R = wx.shape[0], wdt.shape[1]
+        dt = xc.dtype
+        if g_delta is None:
+            g_delta = torch.zeros(D, T, device=xc.device, dtype=dt)
+        g_delta = _hip_rows(g_delta.to(dt), 8, "MixerProjFn")
+        g_xd = _hip_rows(g_xd.to(dt), 8, "MixerProjFn") if g_xd is not None else None
+        du = ctx.handoff.take() if ctx.handoff is not None else None
+        if du is not None:
+            du = du.transpose(0, 1)                          # (B, D, L) channel-major -> (D, B, L)
+            du = du.reshape(D, T) if du.is_contiguous() else du.reshape(D, T).contiguous()
+            du = du.to(dt)
+        dxd = torch.empty(P, T, device=xc.device, dtype=dt)
+        dx = torch.empty(D, T, device=xc.device, dtype=dt)
+        p = _lib.MixerProjBwdParams()
+        p.dim, p.tokens, p.rank, p.proj_rows, p.dtype = D, T, R, P, _lib.dtype_code(dt)
+        p.g_delta_ld, p.d_x_dbl_ld, p.dx_ld = g_delta.stride(0), T, T
+        p.g_delta, p.w_x, p.w_dt, p.d_x_dbl, p.dx = g_delta.data_ptr(), wx.data_ptr(), wdt.data_ptr(), dxd.data_ptr(), dx.data_ptr()
+        if g_xd is not None:
+            p.g_x_dbl, p.g_x_dbl_ld = g_xd.data_ptr(), g_xd.stride(0)
+        if du is not None:
+            p.du, p.du_ld = du.data_ptr(), du.stride(0)
+        _lib.check(lib.mc_mixer_proj_bwd(ctypes.byref(p), _lib.stream_handle(xc.device)), "mc_mixer_proj_bwd")
+        dw_x = wgrad(dxd, xc.t()) if ctx.needs_input_grad[1] else None
+        dw_dt = wgrad(g_delta, xd[:R].t()) if ctx.needs_input_grad[2] else None
+        return (dx if ctx.needs_input_grad[0] else None), dw_x, dw_dt, None
+
+
+def mixer_proj(x_cm, w_x, w_dt, handoff=None):
+    """(x_dbl (P, T), delta (D, T)) for the mixer's channel-major x (D, T); see MixerProjFn."""
+    return MixerProjFn.apply(x_cm, w_x, w_dt, handoff)
+
+
 # ---------------------------------------------------------------------------- fused bias-gradient passes (mc_ops.h)
 def _aligned_rows(t, V):
     return t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and t.stride(0) % V == 0

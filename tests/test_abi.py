@@ -120,7 +120,9 @@ def test_attention_validation_without_launch():
                                           ("mc_ss2d_conv_bwd_params", "SS2DConvBwdParams"),
                                           ("mc_ss2d_merge_params", "SS2DMergeParams"),
                                           ("mc_ss2d_merge_bwd_params", "SS2DMergeBwdParams"),
-                                          ("mc_patch_input_params", "PatchInputParams")])
+                                          ("mc_patch_input_params", "PatchInputParams"),
+                                          ("mc_mixer_proj_params", "MixerProjParams"),
+                                          ("mc_mixer_proj_bwd_params", "MixerProjBwdParams")])
 def test_struct_layout_matches_header(cname, pyname):
     from mamba_clip_amd import _lib
     cls = getattr(_lib, pyname)
