@@ -160,7 +160,7 @@ int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, void* dst_ba
  * (dim, tokens), tokens contiguous; all 16-bit (dtype bf16 / f16), weights contiguous.
  *   forward:  x_dbl (P, T) = w_x (P, D) . x (D, T), rounded to dtype;
  *             delta (D, T) = w_dt (D, R) . x_dbl[0:R], rounded (no bias: the scan adds it)
- *   backward: d_x_dbl (P, T) = [w_dt^T . g_delta + g_x_dbl[0:R] ; g_x_dbl[R:P]], rounded;
+ *   backward: d_x_dbl (P, T) = [w_dt^T . g_delta ; g_b ; g_c], rounded;
  *             dx (D, T) = w_x^T . d_x_dbl + du (du nullable), rounded once
  * The weight gradients are left to the caller (they are reductions over T).
  * Requirements: dim % 64 == 0, tokens % 8 == 0, rank % 16 == 0 in [16, 96], proj_rows = rank + 32
@@ -180,9 +180,10 @@ int mc_mixer_proj_fwd(const mc_mixer_proj_params* p, void* stream);
 
 typedef struct mc_mixer_proj_bwd_params {
   int32_t dim, tokens, rank, proj_rows, dtype;
-  int64_t g_delta_ld, g_x_dbl_ld, du_ld, d_x_dbl_ld, dx_ld;
+  int64_t g_delta_ld, g_b_ld, g_c_ld, du_ld, d_x_dbl_ld, dx_ld;
   const void* g_delta;                    /* (dim, tokens): gradient of delta */
-  const void* g_x_dbl;                    /* nullable (proj_rows, tokens): gradient of x_dbl (dB / dC rows) */
+  const void* g_b;                        /* nullable (16, tokens): gradient of x_dbl's B rows (the scan's dB) */
+  const void* g_c;                        /* nullable (16, tokens): gradient of the C rows (dC) */
   const void* w_x;
   const void* w_dt;
   const void* du;                         /* nullable (dim, tokens): the other consumer's gradient of x */

@@ -17,7 +17,8 @@
 //    dt_raw^T Wdt^T on MFMA with the token on the accumulator rows, so each lane holds 4 consecutive
 //    tokens of one channel; staged per wave in LDS and written as 128-B channel-row pieces.
 //  * backward: d_dtraw (R x 64) over 64-channel chunks of ddelta (Wdt chunk and ddelta chunk in
-//    LDS), rounded, joined with the dB / dC rows into d_xdbl (written out for the weight gradients);
+//    LDS), rounded, joined with the scan's dB / dC rows into d_xdbl (written out for the weight
+//    gradients: the B / C outputs are separate autograd outputs, so no zero-filled x_dbl gradient);
 //    dx^T = d_xdbl^T Wx over 64-channel chunks of Wx (LDS), + du in the epilogue, 128-B row pieces.
 // Bytes per token tile (C2, D 1536, P 80, R 48): forward reads 192 KB and writes 202 KB; backward reads
 // 394 KB and writes 202 KB.  The weight gradients stay split-K library GEMMs (ops.wgrad): fused, each
@@ -63,10 +64,10 @@ __device__ __forceinline__ uint16_t h16(float x) { return (uint16_t)bits16<TI>(x
 struct Args {
   int D, T, R, P;
   int64_t x_ld, xd_ld, dl_ld;              // forward: x, x_dbl, delta row strides
-  int64_t gd_ld, gx_ld, du_ld, dxd_ld, dx_ld;   // backward
+  int64_t gd_ld, gb_ld, gc_ld, du_ld, dxd_ld, dx_ld;   // backward
   const void* x; const void* wx; const void* wdt;
   void* xd; void* dl;
-  const void* gd; const void* gx; const void* du;
+  const void* gd; const void* gb; const void* gc; const void* du;
   void* dxd; void* dx;
 };
 
@@ -271,24 +272,20 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
       if (kc + 1 < nk) park_chunk(buf ^ 1);
       __syncthreads();
     }
-    // rows 0 .. R-1 of d_xdbl: d_dtraw (+ any direct gradient of the dt_raw rows), rounded as the
-    // dt_proj input-gradient GEMM stores it; rows R .. P-1: dB / dC as given
-    const TI* gx = reinterpret_cast<const TI*>(a.gx);
+    // rows 0 .. R-1 of d_xdbl: d_dtraw, rounded as the dt_proj input-gradient GEMM stores it;
+    // rows R .. P-1: dB / dC as given (16 rows each)
 #pragma unroll
     for (int m = 0; m < RT; ++m) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 16 * m + 4 * g + j, t = t0 + 16 * w + li;
-          float v = acc[m][j];
-          if (gx && t < a.T) v += to_f(gx[(int64_t)r * a.gx_ld + t]);
-          sdx[r * kLS + 16 * w + li] = h16<TI>(v);
-        }
+        for (int j = 0; j < 4; ++j) sdx[(16 * m + 4 * g + j) * kLS + 16 * w + li] = h16<TI>(acc[m][j]);
       }
     for (int q = tid; q < (P - R) * 8; q += kThreads) {
-      const int row = R + (q >> 3), cp = q & 7;
+      const int row = q >> 3, cp = q & 7;   // row of the B / C block (0 .. 31)
+      const TI* src = reinterpret_cast<const TI*>(row < 16 ? a.gb : a.gc);
+      const int64_t ld = row < 16 ? a.gb_ld : a.gc_ld;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (gx && t0 + 8 * cp < a.T) v = *reinterpret_cast<const uint4*>(gx + (int64_t)row * a.gx_ld + t0 + 8 * cp);
-      *reinterpret_cast<uint4*>(sdx + row * kLS + 8 * cp) = v;
+      if (src && t0 + 8 * cp < a.T) v = *reinterpret_cast<const uint4*>(src + (int64_t)(row & 15) * ld + t0 + 8 * cp);
+      *reinterpret_cast<uint4*>(sdx + (R + row) * kLS + 8 * cp) = v;
     }
   }
   __syncthreads();
@@ -440,7 +437,8 @@ extern "C" int mc_mixer_proj_bwd(const mc_mixer_proj_bwd_params* p, void* stream
   if (p->tokens == 0) return MC_OK;
   MC_CHECK(p->g_delta && p->w_x && p->w_dt && p->d_x_dbl && p->dx, MC_ERR_INVALID, "mc_mixer_proj_bwd: null pointer");
   MC_CHECK(a16(p->g_delta) && a16(p->d_x_dbl) && a16(p->dx) && a16(p->w_x) && a16(p->w_dt) &&
-               (!p->g_x_dbl || (a16(p->g_x_dbl) && p->g_x_dbl_ld % 8 == 0 && p->g_x_dbl_ld >= p->tokens)) &&
+               (!p->g_b || (a16(p->g_b) && p->g_b_ld % 8 == 0 && p->g_b_ld >= p->tokens)) &&
+               (!p->g_c || (a16(p->g_c) && p->g_c_ld % 8 == 0 && p->g_c_ld >= p->tokens)) &&
                (!p->du || ((reinterpret_cast<uintptr_t>(p->du) & 7) == 0 && p->du_ld % 4 == 0 && p->du_ld >= p->tokens)) &&
                p->g_delta_ld % 8 == 0 && p->d_x_dbl_ld % 8 == 0 && p->dx_ld % 8 == 0 && p->g_delta_ld >= p->tokens &&
                p->d_x_dbl_ld >= p->tokens && p->dx_ld >= p->tokens &&
@@ -448,8 +446,10 @@ extern "C" int mc_mixer_proj_bwd(const mc_mixer_proj_bwd_params* p, void* stream
            MC_ERR_INVALID, "mc_mixer_proj_bwd: 16-B aligned rows (du: 8-B), strides >= tokens, 32-bit spans");
   Args a{};
   a.D = p->dim; a.T = p->tokens; a.R = p->rank; a.P = p->proj_rows;
-  a.gd_ld = p->g_delta_ld; a.gx_ld = p->g_x_dbl_ld; a.du_ld = p->du_ld; a.dxd_ld = p->d_x_dbl_ld; a.dx_ld = p->dx_ld;
-  a.wx = p->w_x; a.wdt = p->w_dt; a.gd = p->g_delta; a.gx = p->g_x_dbl; a.du = p->du; a.dxd = p->d_x_dbl; a.dx = p->dx;
+  a.gd_ld = p->g_delta_ld; a.gb_ld = p->g_b_ld; a.gc_ld = p->g_c_ld; a.du_ld = p->du_ld; a.dxd_ld = p->d_x_dbl_ld;
+  a.dx_ld = p->dx_ld;
+  a.wx = p->w_x; a.wdt = p->w_dt; a.gd = p->g_delta; a.gb = p->g_b; a.gc = p->g_c; a.du = p->du; a.dxd = p->d_x_dbl;
+  a.dx = p->dx;
   hipStream_t s = (hipStream_t)stream;
   if (p->dtype == MC_DTYPE_BF16) launch_t<bf16_t>(false, a, s);
   else launch_t<f16_t>(false, a, s);

@@ -84,8 +84,9 @@ class MixerProjBwdParams(ctypes.Structure):
     """Mirror of ``mc_mixer_proj_bwd_params`` (include/mc_ops.h)."""
     _fields_ = [
         ("dim", c_i32), ("tokens", c_i32), ("rank", c_i32), ("proj_rows", c_i32), ("dtype", c_i32),
-        ("g_delta_ld", c_i64), ("g_x_dbl_ld", c_i64), ("du_ld", c_i64), ("d_x_dbl_ld", c_i64), ("dx_ld", c_i64),
-        ("g_delta", c_vp), ("g_x_dbl", c_vp), ("w_x", c_vp), ("w_dt", c_vp), ("du", c_vp),
+        ("g_delta_ld", c_i64), ("g_b_ld", c_i64), ("g_c_ld", c_i64), ("du_ld", c_i64), ("d_x_dbl_ld", c_i64),
+        ("dx_ld", c_i64),
+        ("g_delta", c_vp), ("g_b", c_vp), ("g_c", c_vp), ("w_x", c_vp), ("w_dt", c_vp), ("du", c_vp),
         ("d_x_dbl", c_vp), ("dx", c_vp),
     ]
 

@@ -121,9 +121,9 @@ class MambaMixer(nn.Module):
             # x_proj and dt_proj in one pass over x (and one backward pass over ddelta that also adds
             # the scan's du into dx: ops.GradHandoff)
             hand = GradHandoff() if (self.du_handoff and x.requires_grad) else None
-            x_dbl, delta = mixer_proj(x_cm, self.x_proj.weight, self.dt_proj.weight, hand)
-            Bm = x_dbl[R:R + N].view(N, Bsz, L).transpose(0, 1)                # (B, N, L)
-            Cm = x_dbl[R + N:].view(N, Bsz, L).transpose(0, 1)
+            Brows, Crows, delta = mixer_proj(x_cm, self.x_proj.weight, self.dt_proj.weight, hand)
+            Bm = Brows.view(N, Bsz, L).transpose(0, 1)                         # (B, N, L)
+            Cm = Crows.view(N, Bsz, L).transpose(0, 1)
             delta = delta.view(di, Bsz, L).transpose(0, 1)
             y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz, hand)
         else:

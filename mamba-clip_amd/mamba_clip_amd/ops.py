@@ -923,10 +923,12 @@ class MixerProjFn(torch.autograd.Function):
         _lib.check(lib.mc_mixer_proj_fwd(ctypes.byref(p), _lib.stream_handle(xc.device)), "mc_mixer_proj_fwd")
         ctx.save_for_backward(xc, wx, wdt, xd)
         ctx.handoff = handoff
-        return xd, delta
+        # B and C rows as their own outputs (views of x_dbl): their gradients arrive separately, so
+        # autograd never builds a zero-filled (P, T) gradient of x_dbl
+        return xd[R:P - 16], xd[P - 16:], delta
 
     @staticmethod
-    def backward(ctx, g_xd, g_delta):
+    def backward(ctx, g_b, g_c, g_delta):
         xc, wx, wdt, xd = ctx.saved_tensors
         lib = _lib.load()
         D, T = xc.shape
@@ -935,7 +937,8 @@ class MixerProjFn(torch.autograd.Function):
         if g_delta is None:
             g_delta = torch.zeros(D, T, device=xc.device, dtype=dt)
         g_delta = _hip_rows(g_delta.to(dt), 8, "MixerProjFn")
-        g_xd = _hip_rows(g_xd.to(dt), 8, "MixerProjFn") if g_xd is not None else None
+        g_b = _hip_rows(g_b.to(dt), 8, "MixerProjFn") if g_b is not None else None
+        g_c = _hip_rows(g_c.to(dt), 8, "MixerProjFn") if g_c is not None else None
         du = ctx.handoff.take() if ctx.handoff is not None else None
         if du is not None:
             du = du.transpose(0, 1)                          # (B, D, L) channel-major -> (D, B, L)
@@ -947,8 +950,10 @@ class MixerProjFn(torch.autograd.Function):
         p.dim, p.tokens, p.rank, p.proj_rows, p.dtype = D, T, R, P, _lib.dtype_code(dt)
         p.g_delta_ld, p.d_x_dbl_ld, p.dx_ld = g_delta.stride(0), T, T
         p.g_delta, p.w_x, p.w_dt, p.d_x_dbl, p.dx = g_delta.data_ptr(), wx.data_ptr(), wdt.data_ptr(), dxd.data_ptr(), dx.data_ptr()
-        if g_xd is not None:
-            p.g_x_dbl, p.g_x_dbl_ld = g_xd.data_ptr(), g_xd.stride(0)
+        if g_b is not None:
+            p.g_b, p.g_b_ld = g_b.data_ptr(), g_b.stride(0)
+        if g_c is not None:
+            p.g_c, p.g_c_ld = g_c.data_ptr(), g_c.stride(0)
         if du is not None:
             p.du, p.du_ld = du.data_ptr(), du.stride(0)
         _lib.check(lib.mc_mixer_proj_bwd(ctypes.byref(p), _lib.stream_handle(xc.device)), "mc_mixer_proj_bwd")
@@ -958,7 +963,8 @@ class MixerProjFn(torch.autograd.Function):
 
 
 def mixer_proj(x_cm, w_x, w_dt, handoff=None):
-    """(x_dbl (P, T), delta (D, T)) for the mixer's channel-major x (D, T); see MixerProjFn."""
+    """(B rows (16, T), C rows (16, T), delta (D, T)) for the mixer's channel-major x (D, T): the
+    x_dbl = [dt_raw; B; C] split of x_proj with dt_raw consumed by dt_proj inside; see MixerProjFn."""
     return MixerProjFn.apply(x_cm, w_x, w_dt, handoff)
 
 

@@ -30,7 +30,7 @@ def test_mixer_proj_fwd_bwd_matches_gemm_chain(shape, dtype):
     wx = torch.randn(P, D, generator=g) * D ** -0.5
     wdt = torch.randn(D, R, generator=g) * R ** -0.5
     gxd = torch.randn(P, T, generator=g).to(dtype)
-    gxd[:R] = 0                                   # dt_raw only feeds dt_proj (as in the mixer)
+    gxd[:R] = 0                                   # dt_raw only feeds dt_proj inside the op
     gdl = torch.randn(D, T, generator=g).to(dtype)
     du = torch.randn(D, T, generator=g).to(dtype)
     # device run (weights as fp32 parameters, cast to the dtype like autocast)
@@ -38,10 +38,12 @@ def test_mixer_proj_fwd_bwd_matches_gemm_chain(shape, dtype):
     wxg, wdtg = wx.to(DEV).requires_grad_(True), wdt.to(DEV).requires_grad_(True)
     hand = GradHandoff()
     with torch.autocast("cuda", dtype=dtype):
-        xd, dl = mixer_proj(xg, wxg, wdtg, hand)
-    assert xd.dtype == dtype and dl.dtype == dtype and xd.shape == (P, T) and dl.shape == (D, T)
+        gb_rows, gc_rows, dl = mixer_proj(xg, wxg, wdtg, hand)
+    assert dl.dtype == dtype and gb_rows.shape == (16, T) and gc_rows.shape == (16, T) and dl.shape == (D, T)
+    xd = gb_rows._base                                     # the whole x_dbl (P, T) the rows view
+    assert xd is not None and xd.shape == (P, T)
     hand.du = du.to(DEV).view(D, 1, T).transpose(0, 1)     # the scan parks du as (B, D, L): here B = 1
-    torch.autograd.backward([xd, dl], [gxd.to(DEV), gdl.to(DEV)])
+    torch.autograd.backward([gb_rows, gc_rows, dl], [gxd[R:R + 16].to(DEV), gxd[R + 16:].to(DEV), gdl.to(DEV)])
     assert hand.du is None
     # fp64 chain on the same 16-bit operands, each product rounded once to the dtype
     x64, wx64, wdt64 = x.double(), wx.to(dtype).double(), wdt.to(dtype).double()
