@@ -13,6 +13,7 @@
 All launches go on the current HIP stream; nothing synchronises.
 """
 import ctypes
+import os
 
 import torch
 
@@ -796,6 +797,20 @@ class weight_cast_scope:
         return False
 
 
+# Input gradients dx = g @ w of the towers' projections with the weight TRANSPOSED first: hipBLASLt
+# runs the "tn" form of these shapes (the forward's) faster than the "nn" form torch picks for a
+# row-major w -- e.g. the ViT fc2 input gradient (50432 x 3072 x 768): 0.246 ms nn vs 0.188 ms tn in
+# the tuning file (tuning/gemm_gfx950_dp.csv); a 16-bit transpose of w is ~5 us.  A/B toggle.
+DGRAD_TN = os.environ.get("MAMBA_CLIP_AMD_DGRAD_TN", "1") != "0"
+
+
+def _dgrad(g2, wc):
+    """g2 (M, N) @ wc (N, K) for a row-major weight copy wc."""
+    if DGRAD_TN and g2.is_cuda and g2.shape[0] >= 8192 and wc.shape[0] * wc.shape[1] >= 1 << 19:
+        return torch.mm(g2, wc.t().contiguous().t())
+    return torch.mm(g2, wc)
+
+
 def _compute_dtype(t):
     if t.is_cuda and torch.is_autocast_enabled("cuda"):
         return torch.get_autocast_dtype("cuda")
@@ -830,7 +845,7 @@ class LinearSK(torch.autograd.Function):
                 # backward needs no transpose copy
                 dx = torch.mm(wc.t(), g2.t()).t()
             else:
-                dx = torch.mm(g2, wc).view(xc.shape)
+                dx = _dgrad(g2, wc).view(xc.shape)
         if ctx.needs_input_grad[1]:
             dw = wgrad(g2.t(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -1019,7 +1034,7 @@ class FC1GeluFn(torch.autograd.Function):
             gh = torch.ops.aten.gelu_backward(g2, h2)
             db = gh.sum(0, dtype=torch.float32)
         x2 = xc.reshape(-1, xc.shape[-1])
-        dx = torch.mm(gh, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(gh, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
         dw = wgrad(gh.t(), x2) if ctx.needs_input_grad[1] else None
         return dx, dw, db if ctx.needs_input_grad[2] else None
 
@@ -1078,7 +1093,7 @@ class QKVProjFn(torch.autograd.Function):
         else:   # CPU tensors (the CPU restatement tests): the same math in torch
             g2 = torch.stack([g.transpose(1, 2) for g in grads], dim=2).reshape(Bsz * N, 3 * C)
             db = g2.sum(0, dtype=torch.float32)
-        dx = torch.mm(g2, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(g2, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
         dw = wgrad(g2.t(), xc.reshape(-1, C)) if ctx.needs_input_grad[1] else None
         return dx, dw, db if ctx.needs_input_grad[2] else None, None
 
