@@ -57,11 +57,13 @@ def test_mixer_proj_fwd_bwd_matches_gemm_chain(shape, dtype):
     dxd_r = dxd_exact.to(dtype).double()
     dx_exact = wx64.t() @ dxd_r + du.double()
     assert ((xg.grad.cpu().double() - dx_exact).abs() <= _bound(dx_exact, dtype) + 2e-3 * float(dx_exact.abs().max())).all()
-    # weight gradients (fp32 from the 16-bit operands)
+    # weight gradients: ops.wgrad, as in the library chain (fp32 split-K sums at T >= 8192; below that
+    # one 16-bit GEMM, so one 16-bit rounding)
     dwx_exact = dxd_r @ x64.t()
     dwdt_exact = gdl.double() @ xd_got[:R].double().t()
+    rt = 1e-3 if T >= 8192 else 2.0 ** -7
     torch.testing.assert_close(wxg.grad.cpu().double(), dwx_exact, rtol=2e-2, atol=2e-2 * float(dwx_exact.abs().max()))
-    torch.testing.assert_close(wdtg.grad.cpu().double(), dwdt_exact, rtol=1e-3, atol=1e-3 * float(dwdt_exact.abs().max()))
+    torch.testing.assert_close(wdtg.grad.cpu().double(), dwdt_exact, rtol=rt, atol=rt * float(dwdt_exact.abs().max()))
 
 
 def test_mixer_proj_rejects_bad_shapes():
