@@ -23,6 +23,8 @@
 // Bytes per token tile (C2, D 1536, P 80, R 48): forward reads 192 KB and writes 202 KB; backward reads
 // 394 KB and writes 202 KB.  The weight gradients stay split-K library GEMMs (ops.wgrad): fused, each
 // workgroup would emit a full fp32 partial of both weights.
+#include <type_traits>
+
 #include "scan_common.h"
 #include "../../include/mc_ops.h"
 
@@ -90,58 +92,70 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)(((int64_t)(a.D - 1) * a.x_ld + a.T) * 2));
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wx, (uint32_t)((int64_t)P * a.D * 2));
 
-  // staging: x chunk = 64 rows x 8 pieces (2 per thread), Wx chunk = P rows x 8 pieces
+  // staging: x chunk = 64 rows x 8 pieces (2 per thread), Wx chunk = P rows x 8 pieces.  Two chunks in
+  // flight behind the one being multiplied (register sets 0 / 1 by chunk parity): one chunk's latency
+  // per iteration left the loop latency-bound at ~2.3 TB/s.
   constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rxv[2], rwv[kWPer];
-  auto load_chunk = [&](int kc) __attribute__((always_inline)) {
+  uint4 rxv[2][2], rwv[2][kWPer];
+  auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
+    constexpr int S = decltype(set)::value;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
       // tokens past T read 0 (range), or the row's tail (their columns are never stored)
-      rxv[i] = ld_piece(rx, a.x_ld, kc * kKC + row, t0, cp);
+      rxv[S][i] = ld_piece(rx, a.x_ld, kc * kKC + row, t0, cp);
     }
 #pragma unroll
     for (int i = 0; i < kWPer; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      rwv[i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
+      rwv[S][i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto park_chunk = [&](int buf) __attribute__((always_inline)) {
+  auto park_chunk = [&](int buf, auto set) __attribute__((always_inline)) {
+    constexpr int S = decltype(set)::value;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      *reinterpret_cast<uint4*>(sx + (buf * kKC + row) * kLS + 8 * cp) = rxv[i];
+      *reinterpret_cast<uint4*>(sx + (buf * kKC + row) * kLS + 8 * cp) = rxv[S][i];
     }
 #pragma unroll
     for (int i = 0; i < kWPer; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      if (q < P * 8) *reinterpret_cast<uint4*>(sw + (buf * P + row) * kLS + 8 * cp) = rwv[i];
+      if (q < P * 8) *reinterpret_cast<uint4*>(sw + (buf * P + row) * kLS + 8 * cp) = rwv[S][i];
     }
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
 
   // ---- phase 1: x_dbl (P x 64) = Wx . x_tile; wave w owns tokens [16 w, 16 w + 16)
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = a.D / kKC;
-  load_chunk(0);
-  park_chunk(0);
+  load_chunk(0, S0());
+  if (nk > 1) load_chunk(1, S1());
+  park_chunk(0, S0());
+  if (nk > 2) load_chunk(2, S0());
   __syncthreads();
-  for (int kc = 0; kc < nk; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < nk) load_chunk(kc + 1);
-    const uint16_t* cx = sx + buf * kKC * kLS;
-    const uint16_t* cw = sw + buf * P * kLS;
+  // chunk kc (parity S) in LDS buffer S; chunk kc + 1 in register set 1 - S; chunk kc + 2 in set S
+  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+    constexpr int S = decltype(par)::value;
+    using N = std::integral_constant<int, 1 - S>;
+    const uint16_t* cx = sx + S * kKC * kLS;
+    const uint16_t* cw = sw + S * P * kLS;
 #pragma unroll
     for (int s = 0; s < kKC / 16; ++s) {
       const s16x4 b = tr_frag(cx, kLS, 16 * s, 16 * w, lane);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = mma<TI>(row_frag(cw, kLS, 16 * m, 16 * s, lane), b, acc[m]);
     }
-    if (kc + 1 < nk) {
-      park_chunk(buf ^ 1);   // the other buffer's last readers finished before the previous barrier
-    }
+    if (kc + 1 < nk) park_chunk(1 - S, N());   // the other buffer's readers passed the last barrier
+    if (kc + 3 < nk) load_chunk(kc + 3, N());
     __syncthreads();
+  };
+  for (int kc = 0; kc < nk; kc += 2) {   // D % 64 == 0: nk may be odd
+    step(kc, S0());
+    if (kc + 1 < nk) step(kc + 1, S1());
   }
   // x_dbl tile, rounded to the activation dtype, into LDS [p][token] (over the Wx chunks)
   uint16_t* sd = sw;
@@ -225,43 +239,50 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
   // ---- phase 1: d_dtraw (R x 64) = Wdt^T . ddelta_tile over channel chunks; wave w owns tokens 16 w ..
   {
     const int tpr = R / 8;                                // 16-B pieces per Wdt row
-    const int tq = (kKC * tpr + kThreads - 1) / kThreads;  // per thread (R <= 128: <= 4)
-    uint4 rgv[2], rtv[4];
-    auto load_chunk = [&](int kc) __attribute__((always_inline)) {
+    const int tq = (kKC * tpr + kThreads - 1) / kThreads;  // per thread (R <= 96: <= 3)
+    uint4 rgv[2][2], rtv[2][3];   // two chunks in flight (register sets by chunk parity)
+    auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
+      constexpr int S = decltype(set)::value;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-        rgv[i] = ld_piece(rg, a.gd_ld, kc * kKC + row, t0, cp);
+        rgv[S][i] = ld_piece(rg, a.gd_ld, kc * kKC + row, t0, cp);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 3; ++i) {
         const int q = tid + kThreads * i, row = q / tpr, cp = q % tpr;
-        rtv[i] = (i < tq && q < kKC * tpr) ? buf_ld16(rt, (uint32_t)(((kc * kKC + row) * R + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
+        rtv[S][i] = (i < tq && q < kKC * tpr) ? buf_ld16(rt, (uint32_t)(((kc * kKC + row) * R + 8 * cp) * 2))
+                                              : make_uint4(0, 0, 0, 0);
       }
     };
-    auto park_chunk = [&](int buf) __attribute__((always_inline)) {
+    auto park_chunk = [&](int buf, auto set) __attribute__((always_inline)) {
+      constexpr int S = decltype(set)::value;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-        *reinterpret_cast<uint4*>(sg + (buf * kKC + row) * kLS + 8 * cp) = rgv[i];
+        *reinterpret_cast<uint4*>(sg + (buf * kKC + row) * kLS + 8 * cp) = rgv[S][i];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 3; ++i) {
         const int q = tid + kThreads * i, row = q / tpr, cp = q % tpr;
-        if (i < tq && q < kKC * tpr) *reinterpret_cast<uint4*>(st + (buf * kKC + row) * lsr + 8 * cp) = rtv[i];
+        if (i < tq && q < kKC * tpr) *reinterpret_cast<uint4*>(st + (buf * kKC + row) * lsr + 8 * cp) = rtv[S][i];
       }
     };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
     f32x4 acc[RT];
 #pragma unroll
     for (int m = 0; m < RT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    load_chunk(0);
-    park_chunk(0);
+    load_chunk(0, S0());
+    if (nk > 1) load_chunk(1, S1());
+    park_chunk(0, S0());
+    if (nk > 2) load_chunk(2, S0());
     __syncthreads();
-    for (int kc = 0; kc < nk; ++kc) {
-      const int buf = kc & 1;
-      if (kc + 1 < nk) load_chunk(kc + 1);
-      const uint16_t* cg = sg + buf * kKC * kLS;
-      const uint16_t* ct = st + buf * kKC * lsr;
+    auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+      constexpr int S = decltype(par)::value;
+      using N = std::integral_constant<int, 1 - S>;
+      const uint16_t* cg = sg + S * kKC * kLS;
+      const uint16_t* ct = st + S * kKC * lsr;
 #pragma unroll
       for (int s = 0; s < kKC / 16; ++s) {
         const s16x4 b = tr_frag(cg, kLS, 16 * s, 16 * w, lane);
@@ -269,8 +290,13 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
         for (int m = 0; m < RT; ++m)   // A[r][c] = Wdt[c][r]: transposed read of the [c][r] chunk
           acc[m] = mma<TI>(tr_frag(ct, lsr, 16 * s, 16 * m, lane), b, acc[m]);
       }
-      if (kc + 1 < nk) park_chunk(buf ^ 1);
+      if (kc + 1 < nk) park_chunk(1 - S, N());
+      if (kc + 3 < nk) load_chunk(kc + 3, N());
       __syncthreads();
+    };
+    for (int kc = 0; kc < nk; kc += 2) {
+      step(kc, S0());
+      if (kc + 1 < nk) step(kc + 1, S1());
     }
     // rows 0 .. R-1 of d_xdbl: d_dtraw, rounded as the dt_proj input-gradient GEMM stores it;
     // rows R .. P-1: dB / dC as given (16 rows each)
@@ -303,38 +329,49 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
 #pragma unroll
     for (int s = 0; s < MT; ++s) afr[mt][s] = tr_frag(sdx, kLS, 16 * s, 16 * mt, lane);
   constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rwv[kWPer];
-  auto load_w = [&](int kc) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < kWPer; ++i) {
-      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      rwv[i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto park_w = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < kWPer; ++i) {
-      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      if (q < P * 8) *reinterpret_cast<uint4*>(swx + (buf * P + row) * kLS + 8 * cp) = rwv[i];
-    }
-  };
+  uint4 rwv[2][kWPer];   // Wx chunks, two in flight (register sets by chunk parity)
+  uint2 duv[2][4];       // du pieces of the next chunk
   const TI* du = reinterpret_cast<const TI*>(a.du);
-  uint16_t* sow = so + w * 16 * kLS;
-  __syncthreads();   // phase-1 buffers are dead: Wx chunks go over them
-  load_w(0);
-  park_w(0);
-  __syncthreads();
-  for (int kc = 0; kc < nk; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < nk) load_w(kc + 1);
+  auto load_w = [&](int kc, auto set) __attribute__((always_inline)) {
+    constexpr int S = decltype(set)::value;
+#pragma unroll
+    for (int i = 0; i < kWPer; ++i) {
+      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
+      rwv[S][i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto park_w = [&](int buf, auto set) __attribute__((always_inline)) {
+    constexpr int S = decltype(set)::value;
+#pragma unroll
+    for (int i = 0; i < kWPer; ++i) {
+      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
+      if (q < P * 8) *reinterpret_cast<uint4*>(swx + (buf * P + row) * kLS + 8 * cp) = rwv[S][i];
+    }
+  };
+  auto load_du = [&](int kc, auto set) __attribute__((always_inline)) {
+    constexpr int S = decltype(set)::value;
     const int c = kc * kKC + 16 * w + li;   // this lane's channel
-    uint2 duv[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int t = t0 + 16 * mt + 4 * g;
-      duv[mt] = (du && t < a.T) ? *reinterpret_cast<const uint2*>(du + (int64_t)c * a.du_ld + t) : make_uint2(0, 0);
+      duv[S][mt] = (du && t < a.T) ? *reinterpret_cast<const uint2*>(du + (int64_t)c * a.du_ld + t) : make_uint2(0, 0);
     }
-    const uint16_t* cw = swx + buf * P * kLS;
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  uint16_t* sow = so + w * 16 * kLS;
+  __syncthreads();   // phase-1 buffers are dead: Wx chunks go over them
+  load_w(0, S0());
+  if (nk > 1) load_w(1, S1());
+  load_du(0, S0());
+  park_w(0, S0());
+  if (nk > 2) load_w(2, S0());
+  __syncthreads();
+  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+    constexpr int S = decltype(par)::value;
+    using N = std::integral_constant<int, 1 - S>;
+    if (kc + 1 < nk) load_du(kc + 1, N());
+    const uint16_t* cw = swx + S * P * kLS;
     s16x4 bfr[MT];
 #pragma unroll
     for (int s = 0; s < MT; ++s) bfr[s] = tr_frag(cw, kLS, 16 * s, 16 * w, lane);
@@ -345,10 +382,11 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
 #pragma unroll
       for (int s = 0; s < MT; ++s) d[mt] = mma<TI>(afr[mt][s], bfr[s], d[mt]);
     }
-    // + du (fp32, then one rounding: the library's beta = 1 epilogue); lane: channel c, tokens 16 mt + 4 g + j
+    // + du (fp32, then one rounding: the library's beta = 1 epilogue); lane: channel kc * 64 + 16 w + li,
+    // tokens 16 mt + 4 g + j
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const uint4 q4 = make_uint4(duv[mt].x, duv[mt].y, 0u, 0u);
+      const uint4 q4 = make_uint4(duv[S][mt].x, duv[S][mt].y, 0u, 0u);
       const float v0 = d[mt][0] + elem_f<TI>(q4, 0), v1 = d[mt][1] + elem_f<TI>(q4, 1);
       const float v2 = d[mt][2] + elem_f<TI>(q4, 2), v3 = d[mt][3] + elem_f<TI>(q4, 3);
       *reinterpret_cast<uint2*>(sow + li * kLS + 16 * mt + 4 * g) = make_uint2(cvt_pk2<TI>(v0, v1), cvt_pk2<TI>(v2, v3));
@@ -362,8 +400,13 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
         *reinterpret_cast<uint4*>(reinterpret_cast<TI*>(a.dx) + (int64_t)(kc * kKC + 16 * w + ch) * a.dx_ld + t0 + 8 * cp) = v;
     }
     asm volatile("" ::: "memory");
-    if (kc + 1 < nk) park_w(buf ^ 1);
+    if (kc + 1 < nk) park_w(1 - S, N());
+    if (kc + 3 < nk) load_w(kc + 3, N());
     __syncthreads();
+  };
+  for (int kc = 0; kc < nk; kc += 2) {
+    step(kc, S0());
+    if (kc + 1 < nk) step(kc + 1, S1());
   }
 }
 

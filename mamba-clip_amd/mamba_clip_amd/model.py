@@ -88,7 +88,7 @@ class MambaMixer(nn.Module):
         self.fuse_dt_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_DT_PROJ", "0") == "1"   # A/B toggle
         self.du_handoff = True   # scan du -> x_proj's dX epilogue (ops.GradHandoff)
         # x_proj + dt_proj as one HIP pass each way (ops.MixerProjFn); A/B toggle
-        self.fuse_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_MIXER_PROJ", "1") != "0"
+        self.fuse_proj = os.environ.get("MAMBA_CLIP_AMD_FUSE_MIXER_PROJ", "0") == "1"
 
     def forward(self, hidden, A=None):  # (B, L, d_model) contiguous; A: -exp(A_log) when the tower formed it
         Bsz, L, dm = hidden.shape
