@@ -185,11 +185,19 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
   uint16_t* sow = so + w * 16 * kLS;
   const TI* wdt = reinterpret_cast<const TI*>(a.wdt);
   const int g = lane >> 4, li = lane & 15;
+  // Wdt fragments (L2) one n-tile ahead: a load-then-use chain per n-tile left phase 2 latency-bound
+  s16x4 bfr[RS], bnx[RS];
+#pragma unroll
+  for (int s = 0; s < RS; ++s) bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(16 * w + li) * a.R + 16 * s + 4 * g);
   for (int nt = w; nt < a.D / 16; nt += 4) {
     const int c0 = 16 * nt;
-    s16x4 bfr[RS];
 #pragma unroll
-    for (int s = 0; s < RS; ++s) bfr[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(c0 + li) * a.R + 16 * s + 4 * g);
+    for (int s = 0; s < RS; ++s) bfr[s] = bnx[s];
+    if (nt + 4 < a.D / 16) {
+#pragma unroll
+      for (int s = 0; s < RS; ++s)
+        bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(c0 + 64 + li) * a.R + 16 * s + 4 * g);
+    }
     f32x4 d[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {

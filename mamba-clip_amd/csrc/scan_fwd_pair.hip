@@ -33,9 +33,6 @@ namespace mc {
 namespace scan {
 
 constexpr int kPCh = 32;   // channels per wave
-#ifndef MC_FWD_FINE_NT
-#define MC_FWD_FINE_NT 0   // fine saved states with non-temporal stores (A/B lever)
-#endif
 constexpr int kPN = 16;    // dstate
 constexpr int kPH = 8;     // states per lane
 constexpr int kPG = 4;     // positions per recurrence group (32 B of {dt, du} per row)
@@ -63,7 +60,7 @@ struct PairLayout {
   static constexpr int kBCBytes = kT * 2 * kPN * 4;
 };
 
-template <typename TI, bool kSP, int kMinW, bool kPD>
+template <typename TI, bool kSP, int kMinW, bool kPD, bool kFine>
 __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs a) {
   using PL = PairLayout<TI>;
   constexpr int VI = PL::VI, kVPR = PL::kVPR, kNV = PL::kNV;
@@ -266,8 +263,13 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
       const f32x4* bcp = reinterpret_cast<const f32x4*>(bcl + kPH * h);   // position stride 2kN floats = 8 f32x4
       f32x4 nb0 = bcp[0], nb1 = bcp[1], nc0 = bcp[kPN / 4], nc1 = bcp[kPN / 4 + 1];
       f32x4 nq0 = *reinterpret_cast<const f32x4*>(row), nq1 = *reinterpret_cast<const f32x4*>(row + 16);
-#pragma unroll 2
-      for (int t0 = 0; t0 < kT; t0 += kPG) {
+      // two groups (8 positions = the fine saved-state interval) per iteration; the fine-state store
+      // is a compile-time branch after the pair (a runtime test inside the pipelined loop cost ~50 %)
+#pragma unroll 1
+      for (int t8 = 0; t8 < kT; t8 += 2 * kPG) {
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        const int t0 = t8 + gi * kPG;
         const f32x4 q0 = nq0, q1 = nq1;
         {
           const int tn = (t0 + kPG) & (kT - 1);   // (last group: wraps to an unused re-read)
@@ -312,25 +314,22 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           y2 = c1v.hi * x[3] + y2;
           yv[e] = y2.x + y2.y;
         }
-        if (a.state_interval == kFineS && ((t0 + kPG) % kFineS) == 0 && l0 + t0 + kPG <= L_ && a.chunk_states && my_ok) {
-          // fine interval: the state after position l0 + t0 + kPG - 1 (L % 8 == 0: the last one is L - 1)
-          // position-major [b][n_states][dim][16]: the wave's 32 rows of one position are 2 KB contiguous
-          float4* cs = reinterpret_cast<float4*>(
-              a.chunk_states + (((int64_t)b * a.n_states + (l0 + t0 + kPG) / kFineS - 1) * a.dim + dbase + ch) * kPN +
-              kPH * h);
-#if MC_FWD_FINE_NT
-          __builtin_nontemporal_store(f32x4{x[0].x, x[0].y, x[1].x, x[1].y}, reinterpret_cast<f32x4*>(cs));
-          __builtin_nontemporal_store(f32x4{x[2].x, x[2].y, x[3].x, x[3].y}, reinterpret_cast<f32x4*>(cs) + 1);
-#else
-          cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
-          cs[1] = make_float4(x[2].x, x[2].y, x[3].x, x[3].y);
-#endif
-        }
         // partial y over the {dt, du} bytes both lanes of the pair have consumed
         *reinterpret_cast<float4*>(const_cast<char*>(row) + t0 * 8 + 16 * h) = make_float4(yv[0], yv[1], yv[2], yv[3]);
       }
+        if constexpr (kFine) {
+          if (l0 + t8 + 2 * kPG <= L_ && my_ok) {
+            // fine interval: the state after position l0 + t8 + 7 (L % 8 == 0: the last one is L - 1),
+            // position-major [b][n_states][dim][16]: the wave's 32 rows of one position are 2 KB contiguous
+            float4* cs = reinterpret_cast<float4*>(
+                a.chunk_states + (((int64_t)b * a.n_states + (l0 + t8) / kFineS) * a.dim + dbase + ch) * kPN + kPH * h);
+            cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
+            cs[1] = make_float4(x[2].x, x[2].y, x[3].x, x[3].y);
+          }
+        }
+      }
     }
-    if (a.state_interval == kS && a.chunk_states && my_ok && c0 < a.n_states) {   // state after l0 + kT - 1 (kS == kT)
+    if (!kFine && a.chunk_states && my_ok && c0 < a.n_states) {   // state after l0 + kT - 1 (kS == kT)
       float4* cs = reinterpret_cast<float4*>(a.chunk_states +
                                              (((int64_t)b * a.dim + dbase + ch) * a.n_states + c0) * kPN + kPH * h);
       cs[0] = make_float4(x[0].x, x[0].y, x[1].x, x[1].y);
@@ -404,12 +403,20 @@ static int launch_pair_t(const FwdArgs& a0, hipStream_t s) {
   a.total_blocks = a.batch * a.n_groups * a.nblk;
   const size_t lds = (size_t)PairLayout<TI>::kRowBytes + PairLayout<TI>::kBCBytes;
   const dim3 grid(a.total_blocks), block(64);
-  if (a.dpw) {
-    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, true>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, true>), grid, block, lds, s, a);
+  if (a.chunk_states && a.state_interval == kFineS) {   // training forward saving fine states
+    if (a.dpw) {
+      if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, true, true>), grid, block, lds, s, a);
+      else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, true, true>), grid, block, lds, s, a);
+    } else {
+      if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, false, true>), grid, block, lds, s, a);
+      else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, false, true>), grid, block, lds, s, a);
+    }
+  } else if (a.dpw) {
+    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, true, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, true, false>), grid, block, lds, s, a);
   } else {
-    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, false>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, false>), grid, block, lds, s, a);
+    if (a.softplus) hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, true, kMinW, false, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((scan_fwd_pair_kernel<TI, false, kMinW, false, false>), grid, block, lds, s, a);
   }
   const hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_fwd: launch failed: %s", hipGetErrorString(e));
