@@ -38,6 +38,8 @@ constexpr int kKC = 64;                 // channels per staged chunk
 constexpr int kLS = kKC + 8;            // LDS row stride in 16-bit elements (144 B: 16-B aligned, bank-skewed)
 constexpr int kPMax = 128;              // x_dbl rows supported (R + 2N)
 constexpr int kThreads = 256;
+constexpr int kDepth = 4;               // K chunks in flight behind the one being multiplied (register sets)
+template <int I> using IC = std::integral_constant<int, I>;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
   // flight behind the one being multiplied (register sets 0 / 1 by chunk parity): one chunk's latency
   // per iteration left the loop latency-bound at ~2.3 TB/s.
   constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rxv[2][2], rwv[2][kWPer];
+  uint4 rxv[kDepth][2], rwv[kDepth][kWPer];
   auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
 #pragma unroll
@@ -124,38 +126,39 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
       if (q < P * 8) *reinterpret_cast<uint4*>(sw + (buf * P + row) * kLS + 8 * cp) = rwv[S][i];
     }
   };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-
   // ---- phase 1: x_dbl (P x 64) = Wx . x_tile; wave w owns tokens [16 w, 16 w + 16)
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = a.D / kKC;
-  load_chunk(0, S0());
-  if (nk > 1) load_chunk(1, S1());
-  park_chunk(0, S0());
-  if (nk > 2) load_chunk(2, S0());
+  // chunk j lives in register set j % kDepth until parked into LDS buffer j % 2
+  load_chunk(0, IC<0>());
+  if (nk > 1) load_chunk(1, IC<1>());
+  if (nk > 2) load_chunk(2, IC<2>());
+  if (nk > 3) load_chunk(3, IC<3>());
+  park_chunk(0, IC<0>());
+  if (nk > 4) load_chunk(4, IC<0>());
   __syncthreads();
-  // chunk kc (parity S) in LDS buffer S; chunk kc + 1 in register set 1 - S; chunk kc + 2 in set S
-  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
-    constexpr int S = decltype(par)::value;
-    using N = std::integral_constant<int, 1 - S>;
-    const uint16_t* cx = sx + S * kKC * kLS;
-    const uint16_t* cw = sw + S * P * kLS;
+  auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
+    constexpr int S = decltype(ph)::value;   // kc % kDepth
+    using N = IC<(S + 1) % kDepth>;
+    const uint16_t* cx = sx + (S & 1) * kKC * kLS;
+    const uint16_t* cw = sw + (S & 1) * P * kLS;
 #pragma unroll
     for (int s = 0; s < kKC / 16; ++s) {
       const s16x4 b = tr_frag(cx, kLS, 16 * s, 16 * w, lane);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = mma<TI>(row_frag(cw, kLS, 16 * m, 16 * s, lane), b, acc[m]);
     }
-    if (kc + 1 < nk) park_chunk(1 - S, N());   // the other buffer's readers passed the last barrier
-    if (kc + 3 < nk) load_chunk(kc + 3, N());
+    if (kc + 1 < nk) park_chunk((S + 1) & 1, N());   // the other buffer's readers passed the last barrier
+    if (kc + kDepth + 1 < nk) load_chunk(kc + kDepth + 1, N());
     __syncthreads();
   };
-  for (int kc = 0; kc < nk; kc += 2) {   // D % 64 == 0: nk may be odd
-    step(kc, S0());
-    if (kc + 1 < nk) step(kc + 1, S1());
+  for (int kc = 0; kc < nk; kc += kDepth) {
+    step(kc, IC<0>());
+    if (kc + 1 < nk) step(kc + 1, IC<1>());
+    if (kc + 2 < nk) step(kc + 2, IC<2>());
+    if (kc + 3 < nk) step(kc + 3, IC<3>());
   }
   // x_dbl tile, rounded to the activation dtype, into LDS [p][token] (over the Wx chunks)
   uint16_t* sd = sw;
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
   {
     const int tpr = R / 8;                                // 16-B pieces per Wdt row
     const int tq = (kKC * tpr + kThreads - 1) / kThreads;  // per thread (R <= 96: <= 3)
-    uint4 rgv[2][2], rtv[2][3];   // two chunks in flight (register sets by chunk parity)
+    uint4 rgv[kDepth][2], rtv[kDepth][3];   // kDepth chunks in flight (register sets by chunk index % kDepth)
     auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
       constexpr int S = decltype(set)::value;
 #pragma unroll
@@ -276,21 +279,21 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
         if (i < tq && q < kKC * tpr) *reinterpret_cast<uint4*>(st + (buf * kKC + row) * lsr + 8 * cp) = rtv[S][i];
       }
     };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
     f32x4 acc[RT];
 #pragma unroll
     for (int m = 0; m < RT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    load_chunk(0, S0());
-    if (nk > 1) load_chunk(1, S1());
-    park_chunk(0, S0());
-    if (nk > 2) load_chunk(2, S0());
+    load_chunk(0, IC<0>());
+    if (nk > 1) load_chunk(1, IC<1>());
+    if (nk > 2) load_chunk(2, IC<2>());
+    if (nk > 3) load_chunk(3, IC<3>());
+    park_chunk(0, IC<0>());
+    if (nk > 4) load_chunk(4, IC<0>());
     __syncthreads();
-    auto step = [&](int kc, auto par) __attribute__((always_inline)) {
-      constexpr int S = decltype(par)::value;
-      using N = std::integral_constant<int, 1 - S>;
-      const uint16_t* cg = sg + S * kKC * kLS;
-      const uint16_t* ct = st + S * kKC * lsr;
+    auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
+      constexpr int S = decltype(ph)::value;
+      using N = IC<(S + 1) % kDepth>;
+      const uint16_t* cg = sg + (S & 1) * kKC * kLS;
+      const uint16_t* ct = st + (S & 1) * kKC * lsr;
 #pragma unroll
       for (int s = 0; s < kKC / 16; ++s) {
         const s16x4 b = tr_frag(cg, kLS, 16 * s, 16 * w, lane);
@@ -298,13 +301,15 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
         for (int m = 0; m < RT; ++m)   // A[r][c] = Wdt[c][r]: transposed read of the [c][r] chunk
           acc[m] = mma<TI>(tr_frag(ct, lsr, 16 * s, 16 * m, lane), b, acc[m]);
       }
-      if (kc + 1 < nk) park_chunk(1 - S, N());
-      if (kc + 3 < nk) load_chunk(kc + 3, N());
+      if (kc + 1 < nk) park_chunk((S + 1) & 1, N());
+      if (kc + kDepth + 1 < nk) load_chunk(kc + kDepth + 1, N());
       __syncthreads();
     };
-    for (int kc = 0; kc < nk; kc += 2) {
-      step(kc, S0());
-      if (kc + 1 < nk) step(kc + 1, S1());
+    for (int kc = 0; kc < nk; kc += kDepth) {
+      step(kc, IC<0>());
+      if (kc + 1 < nk) step(kc + 1, IC<1>());
+      if (kc + 2 < nk) step(kc + 2, IC<2>());
+      if (kc + 3 < nk) step(kc + 3, IC<3>());
     }
     // rows 0 .. R-1 of d_xdbl: d_dtraw, rounded as the dt_proj input-gradient GEMM stores it;
     // rows R .. P-1: dB / dC as given (16 rows each)
@@ -337,8 +342,8 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
 #pragma unroll
     for (int s = 0; s < MT; ++s) afr[mt][s] = tr_frag(sdx, kLS, 16 * s, 16 * mt, lane);
   constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rwv[2][kWPer];   // Wx chunks, two in flight (register sets by chunk parity)
-  uint2 duv[2][4];       // du pieces of the next chunk
+  uint4 rwv[kDepth][kWPer];   // Wx chunks in flight (register sets by chunk index % kDepth)
+  uint2 duv[kDepth][4];       // du pieces, kDepth - 1 chunks ahead
   const TI* du = reinterpret_cast<const TI*>(a.du);
   auto load_w = [&](int kc, auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
@@ -365,21 +370,24 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
       duv[S][mt] = (du && t < a.T) ? *reinterpret_cast<const uint2*>(du + (int64_t)c * a.du_ld + t) : make_uint2(0, 0);
     }
   };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
   uint16_t* sow = so + w * 16 * kLS;
   __syncthreads();   // phase-1 buffers are dead: Wx chunks go over them
-  load_w(0, S0());
-  if (nk > 1) load_w(1, S1());
-  load_du(0, S0());
-  park_w(0, S0());
-  if (nk > 2) load_w(2, S0());
+  load_w(0, IC<0>());
+  if (nk > 1) load_w(1, IC<1>());
+  if (nk > 2) load_w(2, IC<2>());
+  if (nk > 3) load_w(3, IC<3>());
+  load_du(0, IC<0>());
+  if (nk > 1) load_du(1, IC<1>());
+  if (nk > 2) load_du(2, IC<2>());
+  park_w(0, IC<0>());
+  if (nk > 4) load_w(4, IC<0>());
   __syncthreads();
-  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
-    constexpr int S = decltype(par)::value;
-    using N = std::integral_constant<int, 1 - S>;
-    if (kc + 1 < nk) load_du(kc + 1, N());
-    const uint16_t* cw = swx + S * P * kLS;
+  auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
+    constexpr int S = decltype(ph)::value;
+    using N = IC<(S + 1) % kDepth>;
+    using P3 = IC<(S + 3) % kDepth>;
+    if (kc + 3 < nk) load_du(kc + 3, P3());
+    const uint16_t* cw = swx + (S & 1) * P * kLS;
     s16x4 bfr[MT];
 #pragma unroll
     for (int s = 0; s < MT; ++s) bfr[s] = tr_frag(cw, kLS, 16 * s, 16 * w, lane);
@@ -408,13 +416,15 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
         *reinterpret_cast<uint4*>(reinterpret_cast<TI*>(a.dx) + (int64_t)(kc * kKC + 16 * w + ch) * a.dx_ld + t0 + 8 * cp) = v;
     }
     asm volatile("" ::: "memory");
-    if (kc + 1 < nk) park_w(1 - S, N());
-    if (kc + 3 < nk) load_w(kc + 3, N());
+    if (kc + 1 < nk) park_w((S + 1) & 1, N());
+    if (kc + kDepth + 1 < nk) load_w(kc + kDepth + 1, N());
     __syncthreads();
   };
-  for (int kc = 0; kc < nk; kc += 2) {
-    step(kc, S0());
-    if (kc + 1 < nk) step(kc + 1, S1());
+  for (int kc = 0; kc < nk; kc += kDepth) {
+    step(kc, IC<0>());
+    if (kc + 1 < nk) step(kc + 1, IC<1>());
+    if (kc + 2 < nk) step(kc + 2, IC<2>());
+    if (kc + 3 < nk) step(kc + 3, IC<3>());
   }
 }
 
