@@ -38,6 +38,9 @@ constexpr int kKC = 64;                 // channels per staged chunk
 constexpr int kLS = kKC + 8;            // LDS row stride in 16-bit elements (144 B: 16-B aligned, bank-skewed)
 constexpr int kPMax = 128;              // x_dbl rows supported (R + 2N)
 constexpr int kThreads = 256;
+#ifndef MP_EXP
+#define MP_EXP 0   // timing experiments: 1 = forward phase 1 only, 2 = forward phase 2 only (wrong results)
+#endif
 constexpr int kDepth = 4;               // K chunks in flight behind the one being multiplied (register sets)
 template <int I> using IC = std::integral_constant<int, I>;
 
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
     if (kc + kDepth + 1 < nk) load_chunk(kc + kDepth + 1, N());
     __syncthreads();
   };
-  for (int kc = 0; kc < nk; kc += kDepth) {
+  for (int kc = 0; kc < (MP_EXP == 2 ? 0 : nk); kc += kDepth) {
     step(kc, IC<0>());
     if (kc + 1 < nk) step(kc + 1, IC<1>());
     if (kc + 2 < nk) step(kc + 2, IC<2>());
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
   s16x4 bfr[RS], bnx[RS];
 #pragma unroll
   for (int s = 0; s < RS; ++s) bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(16 * w + li) * a.R + 16 * s + 4 * g);
-  for (int nt = w; nt < a.D / 16; nt += 4) {
+  for (int nt = w; nt < (MP_EXP == 1 ? 0 : a.D / 16); nt += 4) {
     const int c0 = 16 * nt;
 #pragma unroll
     for (int s = 0; s < RS; ++s) bfr[s] = bnx[s];
