@@ -37,11 +37,8 @@ constexpr int kTT = 64;                 // tokens per workgroup
 constexpr int kKC = 64;                 // channels per staged chunk
 constexpr int kLS = kKC + 8;            // LDS row stride in 16-bit elements (144 B: 16-B aligned, bank-skewed)
 constexpr int kPMax = 128;              // x_dbl rows supported (R + 2N)
-constexpr int kThreads = 256;
-#ifndef MP_EXP
-#define MP_EXP 0   // timing experiments: 1 = forward phase 1 only, 2 = forward phase 2 only (wrong results)
-#endif
-constexpr int kDepth = 4;               // K chunks in flight behind the one being multiplied (register sets)
+constexpr int kWaves = 8;              // two waves per SIMD per workgroup: the K loops are latency-bound
+constexpr int kThreads = 64 * kWaves;
 template <int I> using IC = std::integral_constant<int, I>;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -84,31 +81,34 @@ __device__ __forceinline__ uint4 ld_piece(__amdgpu_buffer_rsrc_t r, int64_t ld, 
 }
 
 // ---------------------------------------------------------------------------- forward
+// Phase 1: wave w owns token n-tile (w & 3) and k-steps {2 (w >> 2), 2 (w >> 2) + 1} of every 64-channel
+// chunk (the two halves of the workgroup split K and sum through LDS at the end).  Phase 2: wave w owns
+// delta n-tiles w, w + 8, ... with all four token m-tiles.  The next chunk's x / Wx pieces are loaded
+// while the current one is multiplied (register sets by chunk parity).
 template <typename TI, int MT>   // MT = P / 16 x_dbl row tiles
-__global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args a) {
+__global__ __launch_bounds__(kThreads, 1) void mixer_proj_fwd_kernel(const Args a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int P = MT * 16;
   uint16_t* sx = smem;                                   // [2][kKC][kLS]   x chunks
-  uint16_t* sw = sx + 2 * kKC * kLS;                     // [2][P][kLS]     Wx chunks; later x_dbl tile [P][kLS]
-  uint16_t* so = sw + 2 * MT * 16 * kLS;                 // [4 waves][16][kLS] delta staging
+  uint16_t* sw = sx + 2 * kKC * kLS;                     // [2][P][kLS]     Wx chunks; then the x_dbl tile [P][kLS]
+  float* red = reinterpret_cast<float*>(sw + 2 * P * kLS);   // [P][kTT] fp32 K-half partials
+  uint16_t* so = reinterpret_cast<uint16_t*>(red);       // phase 2: [kWaves][16][kLS] delta staging (over red)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int nw = w & 3, kh = w >> 2;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int t0 = tile * kTT;
-  const int P = MT * 16;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)(((int64_t)(a.D - 1) * a.x_ld + a.T) * 2));
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wx, (uint32_t)((int64_t)P * a.D * 2));
 
-  // staging: x chunk = 64 rows x 8 pieces (2 per thread), Wx chunk = P rows x 8 pieces.  Two chunks in
-  // flight behind the one being multiplied (register sets 0 / 1 by chunk parity): one chunk's latency
-  // per iteration left the loop latency-bound at ~2.3 TB/s.
-  constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rxv[kDepth][2], rwv[kDepth][kWPer];
+  constexpr int kWPer = (P * 8 + kThreads - 1) / kThreads;   // Wx pieces per thread
+  uint4 rxv[2], rwv[2][kWPer];
   auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      // tokens past T read 0 (range), or the row's tail (their columns are never stored)
-      rxv[S][i] = ld_piece(rx, a.x_ld, kc * kKC + row, t0, cp);
+    {
+      const int row = tid >> 3, cp = tid & 7;   // 64 rows x 8 pieces: one per thread
+      // tokens past T read 0 (range) or the row's tail (their columns are never stored)
+      rxv[S] = ld_piece(rx, a.x_ld, kc * kKC + row, t0, cp);
     }
 #pragma unroll
     for (int i = 0; i < kWPer; ++i) {
@@ -116,65 +116,70 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
       rwv[S][i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto park_chunk = [&](int buf, auto set) __attribute__((always_inline)) {
+  auto park_chunk = [&](auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      *reinterpret_cast<uint4*>(sx + (buf * kKC + row) * kLS + 8 * cp) = rxv[S][i];
+    {
+      const int row = tid >> 3, cp = tid & 7;
+      *reinterpret_cast<uint4*>(sx + (S * kKC + row) * kLS + 8 * cp) = rxv[S];
     }
 #pragma unroll
     for (int i = 0; i < kWPer; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      if (q < P * 8) *reinterpret_cast<uint4*>(sw + (buf * P + row) * kLS + 8 * cp) = rwv[S][i];
+      if (q < P * 8) *reinterpret_cast<uint4*>(sw + (S * P + row) * kLS + 8 * cp) = rwv[S][i];
     }
   };
-  // ---- phase 1: x_dbl (P x 64) = Wx . x_tile; wave w owns tokens [16 w, 16 w + 16)
+
+  // ---- phase 1: x_dbl (P x 64) = Wx . x_tile
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = a.D / kKC;
-  // chunk j lives in register set j % kDepth until parked into LDS buffer j % 2
   load_chunk(0, IC<0>());
   if (nk > 1) load_chunk(1, IC<1>());
-  if (nk > 2) load_chunk(2, IC<2>());
-  if (nk > 3) load_chunk(3, IC<3>());
-  park_chunk(0, IC<0>());
-  if (nk > 4) load_chunk(4, IC<0>());
+  park_chunk(IC<0>());
+  if (nk > 2) load_chunk(2, IC<0>());
   __syncthreads();
-  auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
-    constexpr int S = decltype(ph)::value;   // kc % kDepth
-    using N = IC<(S + 1) % kDepth>;
-    const uint16_t* cx = sx + (S & 1) * kKC * kLS;
-    const uint16_t* cw = sw + (S & 1) * P * kLS;
+  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+    constexpr int S = decltype(par)::value;   // kc & 1: LDS buffer and register set
+    using N = IC<1 - S>;
+    const uint16_t* cx = sx + S * kKC * kLS;
+    const uint16_t* cw = sw + S * P * kLS;
 #pragma unroll
-    for (int s = 0; s < kKC / 16; ++s) {
-      const s16x4 b = tr_frag(cx, kLS, 16 * s, 16 * w, lane);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int s = 2 * kh + s2;
+      const s16x4 b = tr_frag(cx, kLS, 16 * s, 16 * nw, lane);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = mma<TI>(row_frag(cw, kLS, 16 * m, 16 * s, lane), b, acc[m]);
     }
-    if (kc + 1 < nk) park_chunk((S + 1) & 1, N());   // the other buffer's readers passed the last barrier
-    if (kc + kDepth + 1 < nk) load_chunk(kc + kDepth + 1, N());
+    if (kc + 1 < nk) park_chunk(N());   // buffer 1 - S: its readers passed the last barrier
+    if (kc + 3 < nk) load_chunk(kc + 3, N());
     __syncthreads();
   };
-  for (int kc = 0; kc < (MP_EXP == 2 ? 0 : nk); kc += kDepth) {
+  for (int kc = 0; kc < nk; kc += 2) {
     step(kc, IC<0>());
     if (kc + 1 < nk) step(kc + 1, IC<1>());
-    if (kc + 2 < nk) step(kc + 2, IC<2>());
-    if (kc + 3 < nk) step(kc + 3, IC<3>());
   }
-  // x_dbl tile, rounded to the activation dtype, into LDS [p][token] (over the Wx chunks)
-  uint16_t* sd = sw;
-  {
-    const int g = lane >> 4, li = lane & 15;
+  // K halves summed through LDS (fixed order: half 0 + half 1), rounded to the activation dtype (what
+  // the x_proj GEMM stores), kept as the x_dbl tile [p][token] over the Wx chunks
+  if (kh == 1) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sd[(16 * m + 4 * g + j) * kLS + 16 * w + li] = h16<TI>(acc[m][j]);
+      for (int j = 0; j < 4; ++j) red[(16 * m + 4 * g + j) * kTT + 16 * nw + li] = acc[m][j];
   }
   __syncthreads();
-  // x_dbl to HBM: P rows x 8 pieces
-  for (int q = tid; q < P * 8; q += kThreads) {
+  uint16_t* sd = sw;
+  if (kh == 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * m + 4 * g + j;
+        sd[r * kLS + 16 * nw + li] = h16<TI>(acc[m][j] + red[r * kTT + 16 * nw + li]);
+      }
+  }
+  __syncthreads();
+  for (int q = tid; q < P * 8; q += kThreads) {   // x_dbl to HBM
     const int row = q >> 3, cp = q & 7;
     if (t0 + 8 * cp < a.T)
       *reinterpret_cast<uint4*>(reinterpret_cast<TI*>(a.xd) + row * a.xd_ld + t0 + 8 * cp) =
@@ -190,19 +195,18 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
     for (int s = 0; s < RS; ++s) afr[mt][s] = tr_frag(sd, kLS, 16 * s, 16 * mt, lane);
   uint16_t* sow = so + w * 16 * kLS;
   const TI* wdt = reinterpret_cast<const TI*>(a.wdt);
-  const int g = lane >> 4, li = lane & 15;
-  // Wdt fragments (L2) one n-tile ahead: a load-then-use chain per n-tile left phase 2 latency-bound
+  // Wdt fragments (L2) one n-tile ahead
   s16x4 bfr[RS], bnx[RS];
 #pragma unroll
   for (int s = 0; s < RS; ++s) bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(16 * w + li) * a.R + 16 * s + 4 * g);
-  for (int nt = w; nt < (MP_EXP == 1 ? 0 : a.D / 16); nt += 4) {
+  for (int nt = w; nt < a.D / 16; nt += kWaves) {
     const int c0 = 16 * nt;
 #pragma unroll
     for (int s = 0; s < RS; ++s) bfr[s] = bnx[s];
-    if (nt + 4 < a.D / 16) {
+    if (nt + kWaves < a.D / 16) {
 #pragma unroll
       for (int s = 0; s < RS; ++s)
-        bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(c0 + 64 + li) * a.R + 16 * s + 4 * g);
+        bnx[s] = *reinterpret_cast<const s16x4*>(wdt + (int64_t)(c0 + 16 * kWaves + li) * a.R + 16 * s + 4 * g);
     }
     f32x4 d[4];
 #pragma unroll
@@ -229,20 +233,26 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_fwd_kernel(const Args 
 }
 
 // ---------------------------------------------------------------------------- backward (input gradients)
+// Phase 1 as the forward's (d_dtraw over chunks of ddelta, K halves per wave group).  Phase 2 per 64-channel
+// chunk of Wx: wave w owns channel n-tile (w & 3) and token m-tiles {2 (w >> 2), +1}; the chunk's dx
+// (64 channels x 64 tokens) is staged in LDS and written by all threads as 128-B row pieces.
 template <typename TI, int MT>   // P = 16 MT, R = 16 (MT - 2): dstate 16
-__global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args a) {
+__global__ __launch_bounds__(kThreads, 1) void mixer_proj_bwd_kernel(const Args a) {
   constexpr int RT = MT - 2;
+  constexpr int P = MT * 16;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int R = a.R, P = MT * 16;
+  const int R = a.R;
   const int lsr = R + 8;                                  // Wdt chunk row stride (16-B rows: R % 16 == 0)
   uint16_t* sg = smem;                                   // phase 1: [2][kKC][kLS] ddelta chunks
   uint16_t* st = sg + 2 * kKC * kLS;                     //          [2][kKC][lsr] Wdt chunks
   uint16_t* swx = smem;                                  // phase 2: [2][P][kLS]   Wx column chunks (aliases)
   const int ph1 = 2 * kKC * kLS + 2 * kKC * lsr, ph2 = 2 * P * kLS;
   uint16_t* sdx = smem + (ph1 > ph2 ? ph1 : ph2);        // [P][kLS] d_xdbl tile
-  uint16_t* so = sdx + P * kLS;                          // [4][16][kLS] dx staging
+  float* red = reinterpret_cast<float*>(sdx + P * kLS);  // [R][kTT] fp32 K-half partials
+  uint16_t* stg = reinterpret_cast<uint16_t*>(red);      // phase 2: [2][kKC][kLS] dx staging (over red)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
+  const int nw = w & 3, kh = w >> 2;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int t0 = tile * kTT;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gd, (uint32_t)(((int64_t)(a.D - 1) * a.gd_ld + a.T) * 2));
@@ -250,36 +260,34 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wx, (uint32_t)((int64_t)P * a.D * 2));
   const int nk = a.D / kKC;
 
-  // ---- phase 1: d_dtraw (R x 64) = Wdt^T . ddelta_tile over channel chunks; wave w owns tokens 16 w ..
+  // ---- phase 1: d_dtraw (R x 64) = Wdt^T . ddelta_tile over channel chunks
   {
     const int tpr = R / 8;                                // 16-B pieces per Wdt row
-    const int tq = (kKC * tpr + kThreads - 1) / kThreads;  // per thread (R <= 96: <= 3)
-    uint4 rgv[kDepth][2], rtv[kDepth][3];   // kDepth chunks in flight (register sets by chunk index % kDepth)
+    const int tq = (kKC * tpr + kThreads - 1) / kThreads;  // per thread (R <= 96: <= 2)
+    uint4 rgv[2], rtv[2][2];
     auto load_chunk = [&](int kc, auto set) __attribute__((always_inline)) {
       constexpr int S = decltype(set)::value;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-        rgv[S][i] = ld_piece(rg, a.gd_ld, kc * kKC + row, t0, cp);
+      {
+        const int row = tid >> 3, cp = tid & 7;
+        rgv[S] = ld_piece(rg, a.gd_ld, kc * kKC + row, t0, cp);
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < 2; ++i) {
         const int q = tid + kThreads * i, row = q / tpr, cp = q % tpr;
         rtv[S][i] = (i < tq && q < kKC * tpr) ? buf_ld16(rt, (uint32_t)(((kc * kKC + row) * R + 8 * cp) * 2))
                                               : make_uint4(0, 0, 0, 0);
       }
     };
-    auto park_chunk = [&](int buf, auto set) __attribute__((always_inline)) {
+    auto park_chunk = [&](auto set) __attribute__((always_inline)) {
       constexpr int S = decltype(set)::value;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-        *reinterpret_cast<uint4*>(sg + (buf * kKC + row) * kLS + 8 * cp) = rgv[S][i];
+      {
+        const int row = tid >> 3, cp = tid & 7;
+        *reinterpret_cast<uint4*>(sg + (S * kKC + row) * kLS + 8 * cp) = rgv[S];
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < 2; ++i) {
         const int q = tid + kThreads * i, row = q / tpr, cp = q % tpr;
-        if (i < tq && q < kKC * tpr) *reinterpret_cast<uint4*>(st + (buf * kKC + row) * lsr + 8 * cp) = rtv[S][i];
+        if (i < tq && q < kKC * tpr) *reinterpret_cast<uint4*>(st + (S * kKC + row) * lsr + 8 * cp) = rtv[S][i];
       }
     };
     f32x4 acc[RT];
@@ -287,40 +295,38 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
     for (int m = 0; m < RT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
     load_chunk(0, IC<0>());
     if (nk > 1) load_chunk(1, IC<1>());
-    if (nk > 2) load_chunk(2, IC<2>());
-    if (nk > 3) load_chunk(3, IC<3>());
-    park_chunk(0, IC<0>());
-    if (nk > 4) load_chunk(4, IC<0>());
+    park_chunk(IC<0>());
+    if (nk > 2) load_chunk(2, IC<0>());
     __syncthreads();
-    auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
-      constexpr int S = decltype(ph)::value;
-      using N = IC<(S + 1) % kDepth>;
-      const uint16_t* cg = sg + (S & 1) * kKC * kLS;
-      const uint16_t* ct = st + (S & 1) * kKC * lsr;
+    auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+      constexpr int S = decltype(par)::value;
+      using N = IC<1 - S>;
+      const uint16_t* cg = sg + S * kKC * kLS;
+      const uint16_t* ct = st + S * kKC * lsr;
 #pragma unroll
-      for (int s = 0; s < kKC / 16; ++s) {
-        const s16x4 b = tr_frag(cg, kLS, 16 * s, 16 * w, lane);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int s = 2 * kh + s2;
+        const s16x4 b = tr_frag(cg, kLS, 16 * s, 16 * nw, lane);
 #pragma unroll
         for (int m = 0; m < RT; ++m)   // A[r][c] = Wdt[c][r]: transposed read of the [c][r] chunk
           acc[m] = mma<TI>(tr_frag(ct, lsr, 16 * s, 16 * m, lane), b, acc[m]);
       }
-      if (kc + 1 < nk) park_chunk((S + 1) & 1, N());
-      if (kc + kDepth + 1 < nk) load_chunk(kc + kDepth + 1, N());
+      if (kc + 1 < nk) park_chunk(N());
+      if (kc + 3 < nk) load_chunk(kc + 3, N());
       __syncthreads();
     };
-    for (int kc = 0; kc < nk; kc += kDepth) {
+    for (int kc = 0; kc < nk; kc += 2) {
       step(kc, IC<0>());
       if (kc + 1 < nk) step(kc + 1, IC<1>());
-      if (kc + 2 < nk) step(kc + 2, IC<2>());
-      if (kc + 3 < nk) step(kc + 3, IC<3>());
     }
-    // rows 0 .. R-1 of d_xdbl: d_dtraw, rounded as the dt_proj input-gradient GEMM stores it;
-    // rows R .. P-1: dB / dC as given (16 rows each)
+    // rows 0 .. R-1 of d_xdbl: the K halves summed (half 0 + half 1), rounded as the dt_proj
+    // input-gradient GEMM stores it; rows R .. P-1: dB / dC as given (16 rows each)
+    if (kh == 1) {
 #pragma unroll
-    for (int m = 0; m < RT; ++m) {
+      for (int m = 0; m < RT; ++m)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sdx[(16 * m + 4 * g + j) * kLS + 16 * w + li] = h16<TI>(acc[m][j]);
-      }
+        for (int j = 0; j < 4; ++j) red[(16 * m + 4 * g + j) * kTT + 16 * nw + li] = acc[m][j];
+    }
     for (int q = tid; q < (P - R) * 8; q += kThreads) {
       const int row = q >> 3, cp = q & 7;   // row of the B / C block (0 .. 31)
       const TI* src = reinterpret_cast<const TI*>(row < 16 ? a.gb : a.gc);
@@ -328,6 +334,16 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
       uint4 v = make_uint4(0, 0, 0, 0);
       if (src && t0 + 8 * cp < a.T) v = *reinterpret_cast<const uint4*>(src + (int64_t)(row & 15) * ld + t0 + 8 * cp);
       *reinterpret_cast<uint4*>(sdx + (R + row) * kLS + 8 * cp) = v;
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int m = 0; m < RT; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * m + 4 * g + j;
+          sdx[r * kLS + 16 * nw + li] = h16<TI>(acc[m][j] + red[r * kTT + 16 * nw + li]);
+        }
     }
   }
   __syncthreads();
@@ -338,15 +354,16 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
           *reinterpret_cast<const uint4*>(sdx + row * kLS + 8 * cp);
   }
 
-  // ---- phase 2: dx^T (64 x D) = d_xdbl^T (64 x P) . Wx (P x D) + du^T; wave w owns channels 16 w of each chunk
-  s16x4 afr[4][MT];
+  // ---- phase 2: dx^T (64 x D) = d_xdbl^T (64 x P) . Wx (P x D) + du^T
+  const int mh = kh;   // token half: m-tiles 2 mh, 2 mh + 1
+  s16x4 afr[2][MT];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int s = 0; s < MT; ++s) afr[mt][s] = tr_frag(sdx, kLS, 16 * s, 16 * mt, lane);
-  constexpr int kWPer = (MT * 16 * 8 + kThreads - 1) / kThreads;
-  uint4 rwv[kDepth][kWPer];   // Wx chunks in flight (register sets by chunk index % kDepth)
-  uint2 duv[kDepth][4];       // du pieces, kDepth - 1 chunks ahead
+    for (int s = 0; s < MT; ++s) afr[i][s] = tr_frag(sdx, kLS, 16 * s, 16 * (2 * mh + i), lane);
+  constexpr int kWPer = (P * 8 + kThreads - 1) / kThreads;
+  uint4 rwv[2][kWPer];   // Wx chunks, the next one in flight (register sets by chunk parity)
+  uint2 duv[2][2];       // du pieces, one chunk ahead
   const TI* du = reinterpret_cast<const TI*>(a.du);
   auto load_w = [&](int kc, auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
@@ -356,85 +373,77 @@ __global__ __launch_bounds__(kThreads, 2) void mixer_proj_bwd_kernel(const Args 
       rwv[S][i] = q < P * 8 ? buf_ld16(rw, (uint32_t)((row * a.D + kc * kKC + 8 * cp) * 2)) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto park_w = [&](int buf, auto set) __attribute__((always_inline)) {
+  auto park_w = [&](auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
 #pragma unroll
     for (int i = 0; i < kWPer; ++i) {
       const int q = tid + kThreads * i, row = q >> 3, cp = q & 7;
-      if (q < P * 8) *reinterpret_cast<uint4*>(swx + (buf * P + row) * kLS + 8 * cp) = rwv[S][i];
+      if (q < P * 8) *reinterpret_cast<uint4*>(swx + (S * P + row) * kLS + 8 * cp) = rwv[S][i];
     }
   };
   auto load_du = [&](int kc, auto set) __attribute__((always_inline)) {
     constexpr int S = decltype(set)::value;
-    const int c = kc * kKC + 16 * w + li;   // this lane's channel
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int t = t0 + 16 * mt + 4 * g;
-      duv[S][mt] = (du && t < a.T) ? *reinterpret_cast<const uint2*>(du + (int64_t)c * a.du_ld + t) : make_uint2(0, 0);
-    }
-  };
-  uint16_t* sow = so + w * 16 * kLS;
-  __syncthreads();   // phase-1 buffers are dead: Wx chunks go over them
-  load_w(0, IC<0>());
-  if (nk > 1) load_w(1, IC<1>());
-  if (nk > 2) load_w(2, IC<2>());
-  if (nk > 3) load_w(3, IC<3>());
-  load_du(0, IC<0>());
-  if (nk > 1) load_du(1, IC<1>());
-  if (nk > 2) load_du(2, IC<2>());
-  park_w(0, IC<0>());
-  if (nk > 4) load_w(4, IC<0>());
-  __syncthreads();
-  auto step = [&](int kc, auto ph) __attribute__((always_inline)) {
-    constexpr int S = decltype(ph)::value;
-    using N = IC<(S + 1) % kDepth>;
-    using P3 = IC<(S + 3) % kDepth>;
-    if (kc + 3 < nk) load_du(kc + 3, P3());
-    const uint16_t* cw = swx + (S & 1) * P * kLS;
-    s16x4 bfr[MT];
-#pragma unroll
-    for (int s = 0; s < MT; ++s) bfr[s] = tr_frag(cw, kLS, 16 * s, 16 * w, lane);
-    f32x4 d[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      d[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < MT; ++s) d[mt] = mma<TI>(afr[mt][s], bfr[s], d[mt]);
-    }
-    // + du (fp32, then one rounding: the library's beta = 1 epilogue); lane: channel kc * 64 + 16 w + li,
-    // tokens 16 mt + 4 g + j
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const uint4 q4 = make_uint4(duv[S][mt].x, duv[S][mt].y, 0u, 0u);
-      const float v0 = d[mt][0] + elem_f<TI>(q4, 0), v1 = d[mt][1] + elem_f<TI>(q4, 1);
-      const float v2 = d[mt][2] + elem_f<TI>(q4, 2), v3 = d[mt][3] + elem_f<TI>(q4, 3);
-      *reinterpret_cast<uint2*>(sow + li * kLS + 16 * mt + 4 * g) = make_uint2(cvt_pk2<TI>(v0, v1), cvt_pk2<TI>(v2, v3));
-    }
-    asm volatile("" ::: "memory");
+    const int c = kc * kKC + 16 * nw + li;   // this lane's channel
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int q = lane + 64 * i, ch = q >> 3, cp = q & 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(sow + ch * kLS + 8 * cp);
-      if (t0 + 8 * cp < a.T)
-        *reinterpret_cast<uint4*>(reinterpret_cast<TI*>(a.dx) + (int64_t)(kc * kKC + 16 * w + ch) * a.dx_ld + t0 + 8 * cp) = v;
+      const int t = t0 + 16 * (2 * mh + i) + 4 * g;
+      duv[S][i] = (du && t < a.T) ? *reinterpret_cast<const uint2*>(du + (int64_t)c * a.du_ld + t) : make_uint2(0, 0);
     }
-    asm volatile("" ::: "memory");
-    if (kc + 1 < nk) park_w((S + 1) & 1, N());
-    if (kc + kDepth + 1 < nk) load_w(kc + kDepth + 1, N());
+  };
+  __syncthreads();   // phase-1 buffers and red are dead: Wx chunks / staging go over them
+  load_w(0, IC<0>());
+  if (nk > 1) load_w(1, IC<1>());
+  load_du(0, IC<0>());
+  park_w(IC<0>());
+  if (nk > 2) load_w(2, IC<0>());
+  __syncthreads();
+  auto step = [&](int kc, auto par) __attribute__((always_inline)) {
+    constexpr int S = decltype(par)::value;
+    using N = IC<1 - S>;
+    if (kc + 1 < nk) load_du(kc + 1, N());
+    const uint16_t* cw = swx + S * P * kLS;
+    s16x4 bfr[MT];
+#pragma unroll
+    for (int s = 0; s < MT; ++s) bfr[s] = tr_frag(cw, kLS, 16 * s, 16 * nw, lane);
+    uint16_t* sgt = stg + S * kKC * kLS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < MT; ++s) d = mma<TI>(afr[i][s], bfr[s], d);
+      // + du (fp32, then one rounding: the library's beta = 1 epilogue); lane: channel 16 nw + li of the
+      // chunk, tokens 16 (2 mh + i) + 4 g + j
+      const uint4 q4 = make_uint4(duv[S][i].x, duv[S][i].y, 0u, 0u);
+      const float v0 = d[0] + elem_f<TI>(q4, 0), v1 = d[1] + elem_f<TI>(q4, 1);
+      const float v2 = d[2] + elem_f<TI>(q4, 2), v3 = d[3] + elem_f<TI>(q4, 3);
+      *reinterpret_cast<uint2*>(sgt + (16 * nw + li) * kLS + 16 * (2 * mh + i) + 4 * g) =
+          make_uint2(cvt_pk2<TI>(v0, v1), cvt_pk2<TI>(v2, v3));
+    }
+    __syncthreads();   // the chunk's dx tile is staged
+    {
+      const int row = tid >> 3, cp = tid & 7;   // 64 channels x 8 pieces: one per thread
+      const uint4 v = *reinterpret_cast<const uint4*>(sgt + row * kLS + 8 * cp);
+      if (t0 + 8 * cp < a.T)
+        *reinterpret_cast<uint4*>(reinterpret_cast<TI*>(a.dx) + (int64_t)(kc * kKC + row) * a.dx_ld + t0 + 8 * cp) = v;
+    }
+    if (kc + 1 < nk) park_w(N());   // buffer 1 - S: its readers passed the barrier above
+    if (kc + 3 < nk) load_w(kc + 3, N());
     __syncthreads();
   };
-  for (int kc = 0; kc < nk; kc += kDepth) {
+  for (int kc = 0; kc < nk; kc += 2) {
     step(kc, IC<0>());
     if (kc + 1 < nk) step(kc + 1, IC<1>());
-    if (kc + 2 < nk) step(kc + 2, IC<2>());
-    if (kc + 3 < nk) step(kc + 3, IC<3>());
   }
 }
 
-size_t fwd_lds(int P) { return (size_t)(2 * kKC * kLS + 2 * P * kLS + 4 * 16 * kLS) * 2; }
+size_t fwd_lds(int P) {
+  const size_t red = (size_t)P * kTT * 4, stage = (size_t)kWaves * 16 * kLS * 2;
+  return (size_t)(2 * kKC * kLS + 2 * P * kLS) * 2 + (red > stage ? red : stage);
+}
 size_t bwd_lds(int P, int R) {
   const int ph1 = 2 * kKC * kLS + 2 * kKC * (R + 8), ph2 = 2 * P * kLS;
-  return (size_t)((ph1 > ph2 ? ph1 : ph2) + P * kLS + 4 * 16 * kLS) * 2;
+  const size_t red = (size_t)R * kTT * 4, stage = (size_t)2 * kKC * kLS * 2;
+  return (size_t)((ph1 > ph2 ? ph1 : ph2) + P * kLS) * 2 + (red > stage ? red : stage);
 }
 
 template <typename TI, int MT>
