@@ -145,8 +145,36 @@ def test_c2_mamba130m_mixer_bf16_autocast_vs_fp64():
     hr = h.detach().double().requires_grad_(True)
     ref = R.mamba_mixer_ref(m, hr)
     ref.backward(gy.double())
-    assert _rel(out.float(), ref) < 3e-2
-    assert _rel(h.grad, hr.grad) < 5e-2
+    # vs the fp32-weight model: the bf16 model's own error (weights and activations rounded)
+    e_out, e_grad = _rel(out.float(), ref), _rel(h.grad, hr.grad)
+    # vs the same model with the projection weights rounded to bf16 as autocast rounds them: what is
+    # left is the activations' bf16 storage between the ops
+    hq = h.detach().double().requires_grad_(True)
+    refq = R.mamba_mixer_ref(_bf16_proj_weights(m), hq)
+    refq.backward(gy.double())
+    q_out, q_grad = _rel(out.float(), refq), _rel(h.grad, hq.grad)
+    print(f"bf16 mixer vs fp64: out {e_out:.2e} grad {e_grad:.2e}; vs fp64 with bf16 weights: out {q_out:.2e} "
+          f"grad {q_grad:.2e}")
+    for eo, eg in ((e_out, e_grad), (q_out, q_grad)):
+        assert eo < BF16_MIXER_TOL[0] and eg < BF16_MIXER_TOL[1]
+
+
+# max |err| / max |ref| of the bf16 mixer / 790M layer vs fp64, measured in round 4
+# (profiles/r04/parity/bf16_mixer_tolerances.txt): output 4.5e-3 .. 5.6e-3, input gradient
+# 5.1e-3 .. 7.8e-3, with fp32 or bf16-rounded projection weights alike (the activations' bf16
+# storage between the ops dominates).  Round 3 accepted 3e-2 / 5e-2.
+BF16_MIXER_TOL = (1e-2, 1.2e-2)
+
+
+def _bf16_proj_weights(m):
+    """A copy of mixer m whose Linear weights are rounded to bf16 (what autocast's casts feed the GEMMs)."""
+    import copy
+    mq = copy.deepcopy(m)
+    with torch.no_grad():
+        for mod in mq.modules():
+            if isinstance(mod, torch.nn.Linear):
+                mod.weight.copy_(mod.weight.bfloat16().float())
+    return mq
 
 
 def _mixer_ref_params(m, p, h):
@@ -248,5 +276,12 @@ def test_c4_mamba790m_layer_fwd_bwd():
         normed = R.rmsnorm_ref(hr, None, layer.norm_weight.detach())[0]
         ref = R.mamba_mixer_ref(layer.mixer, normed)
         ref.backward(gy[b:b + 1].double())
-        assert _rel(out[b:b + 1].float(), ref) < 3e-2, b
-        assert _rel(hid.grad[b:b + 1].float(), hr.grad) < 5e-2, b
+        e_out, e_grad = _rel(out[b:b + 1].float(), ref), _rel(hid.grad[b:b + 1].float(), hr.grad)
+        hq = hid[b:b + 1].detach().double().requires_grad_(True)
+        refq = R.mamba_mixer_ref(_bf16_proj_weights(layer.mixer), R.rmsnorm_ref(hq, None, layer.norm_weight.detach())[0])
+        refq.backward(gy[b:b + 1].double())
+        q_out, q_grad = _rel(out[b:b + 1].float(), refq), _rel(hid.grad[b:b + 1].float(), hq.grad)
+        print(f"790M layer row {b}: vs fp64 out {e_out:.2e} grad {e_grad:.2e}; vs fp64 with bf16 weights "
+              f"out {q_out:.2e} grad {q_grad:.2e}")
+        for eo, eg in ((e_out, e_grad), (q_out, q_grad)):
+            assert eo < BF16_MIXER_TOL[0] and eg < BF16_MIXER_TOL[1], b
