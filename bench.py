@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="pairs per GPU")
     ap.add_argument("--model", default="vit_b16-mamba130m")
     ap.add_argument("--scan-iters", type=int, default=20)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: replay the step as one HIP graph (train.GraphedStep; single process), 0: eager, "
+                         "-1: graph when world size is 1 and inputs are resident (default 0 until measured)")
     ap.add_argument("--input", choices=["resident", "host"], default="resident",
                     help="resident: one synthetic batch in HBM (the `value` definition); host: ISIC-shaped raw "
                          "uint8 crops streamed from pinned host memory each step (data.HostToDeviceLoader)")
@@ -288,6 +291,10 @@ def main():
     rank, world = targs.rank, targs.world_size
     gemm_tuned = load_gemm_tuning()               # committed per-shape hipBLASLt/rocBLAS selection
     targs.lr *= world                             # pipeline.py:532
+    use_graph = args.graph == 1 or (args.graph == -1 and world == 1 and args.input == "resident")
+    if use_graph and (world > 1 or args.input != "resident"):
+        raise SystemExit("--graph 1 needs one process and resident inputs")
+    targs.capturable = use_graph
 
     torch.manual_seed(0)
     model = build_clip(args.model).to(device)
@@ -315,6 +322,9 @@ def main():
 
         def step():
             return train_step(model, *next(feed), loss, optimizer, None, targs)
+    elif use_graph:
+        from mamba_clip_amd.train import GraphedStep
+        step = GraphedStep(model, images, texts, targets, loss, optimizer, targs)
     else:
         def step():
             return train_step(model, images, texts, targets, loss, optimizer, None, targs)
@@ -366,6 +376,7 @@ def main():
         "config": {"workload": workload,
                    "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                    "seq_len": seq_len, "image_size": 224, "input": args.input,
+                   "step_launch": "hip-graph replay" if use_graph else "eager",
                    "parallelism": f"dp{world}",
                    "library_gemm_selection": "tunableop-file" if gemm_tuned else "default-heuristic"},
         "mfma_estimate": {"flop_per_pair": flop_pair,

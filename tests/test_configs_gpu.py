@@ -97,7 +97,7 @@ def test_c2_full_size_train_steps():
                            grad_clip_norm=None)
     opt = create_optimizer(model, args)
     images, texts, targets = synthetic_batch(256, 224, 77, model.vocab_size, device=DEV, seed=1000)
-    losses = [float(train_step(model, images, texts, targets, ClipLoss(), opt, None, args)["loss"])
+    losses = [float(train_step(model, images, texts, targets, ClipLoss(), opt, None, args)["loss"].detach())
               for _ in range(3)]
     assert all(math.isfinite(x) for x in losses) and losses[-1] < losses[0], losses
     assert 0.0 <= float(model.logit_scale) <= math.log(100) + 1e-6
