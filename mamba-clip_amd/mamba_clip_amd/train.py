@@ -253,6 +253,9 @@ class GraphedStep:
 
     def __init__(self, model, images, texts, targets, loss, optimizer, args, warmup=3):
         autocast = self.autocast_for(args)
+        # one stream: the towers' two-stream fork / join does not survive capture race-free here (replays
+        # of a two-stream capture differed run to run in round 4's test); replay order = eager order
+        unwrap_model(model).concurrent_towers = False
         run = lambda: train_step(model, images, texts, targets, loss, optimizer, None, args, autocast)  # noqa: E731
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())

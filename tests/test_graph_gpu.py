@@ -29,6 +29,7 @@ def _setup(model_name, batch, seed):
 def test_graphed_step_matches_eager(model_name, batch):
     from mamba_clip_amd.train import GraphedStep, train_step
     m0, o0, l0, a0, (img, txt, tgt) = _setup(model_name, batch, 11)
+    m0.concurrent_towers = False          # GraphedStep captures the towers on one stream
     eager = []
     for _ in range(6):
         eager.append(float(train_step(m0, img, txt, tgt, l0, o0, None, a0, GraphedStep.autocast_for(a0))["loss"].detach()))
