@@ -289,7 +289,7 @@ def main():
                             grad_clip_norm=None, dist_backend="nccl", ddp_static_graph=True, accum_freq=1)
     device = init_device(targs)
     rank, world = targs.rank, targs.world_size
-    gemm_tuned = load_gemm_tuning()               # committed per-shape hipBLASLt/rocBLAS selection
+    gemm_tuned = load_gemm_tuning(model=args.model)   # committed per-shape hipBLASLt/rocBLAS selection
     targs.lr *= world                             # pipeline.py:532
     use_graph = args.graph == 1 or (args.graph == -1 and world == 1 and args.input == "resident")
     if use_graph and (world > 1 or args.input != "resident"):
