@@ -117,7 +117,7 @@ def main(argv=None):
 
     _lib.load()
     device = init_device(args)
-    load_gemm_tuning()
+    load_gemm_tuning(model=getattr(args, "model_stage_1", None) or getattr(args, "model", None))
     torch.manual_seed(args.seed + args.rank)
     model = build_model(args, device)
     inner = model.clip_model if args.stage == 2 else model
