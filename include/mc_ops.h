@@ -154,6 +154,19 @@ typedef struct {
 } mc_cast_chunk;
 int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, void* dst_base, int32_t dst_dtype, void* stream);
 
+/* Transposed 16-bit copies of fp32 weights in one launch (the towers' input gradients run the "tn"
+ * GEMM form, which needs w^T row-major): one table entry per tile of up to 64 x 64 source elements,
+ * dst[c * dst_ld + r] = src[r * src_ld + c] for r < rows, c < cols (src / dst at the tile origins).
+ * tiles: DEVICE array of n_tiles entries. */
+typedef struct mc_cast_t_tile {
+  const float* src;       /* tile origin in the fp32 source */
+  int64_t dst_off;        /* tile origin in dst_base, elements */
+  int32_t src_ld, dst_ld; /* row strides, elements */
+  int32_t rows, cols;     /* tile extent in the source (<= 64 each) */
+} mc_cast_t_tile;
+int mc_cast_transpose_f32_many(int32_t n_tiles, const mc_cast_t_tile* tiles, void* dst_base, int32_t dst_dtype,
+                               void* stream);
+
 /* ---- Mamba mixer projections (mixer_proj.hip): x_proj and dt_proj around the scan, fused.
  * Reference: the mixer's x_dbl = x_proj(x), delta = dt_proj.weight @ dt_raw (upstream
  * mamba_simple.Mamba; SS2D's analogue model.py:519-528, 630-647).  Channel-major activations

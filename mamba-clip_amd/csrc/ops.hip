@@ -1227,6 +1227,62 @@ extern "C" int mc_cast_f32_many(int32_t n_chunks, const mc_cast_chunk* chunks, v
   return check_launch("mc_cast_f32_many");
 }
 
+// ---------------------------------------------------------------------------- transposed weight casts
+namespace {
+template <typename TO>
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const mc_cast_t_tile* __restrict__ tiles, TO* __restrict__ base) {
+  __shared__ float tile[64][65];
+  const mc_cast_t_tile t = tiles[blockIdx.x];
+  const int tid = threadIdx.x, r = tid >> 2, c0 = (tid & 3) * 16;
+  const bool full = t.rows == 64 && t.cols == 64 && (t.src_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(t.src) & 15) == 0;
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(t.src + (int64_t)r * t.src_ld + c0 + 4 * k);
+      tile[r][c0 + 4 * k] = v.x; tile[r][c0 + 4 * k + 1] = v.y; tile[r][c0 + 4 * k + 2] = v.z; tile[r][c0 + 4 * k + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      tile[r][c0 + k] = (r < t.rows && c0 + k < t.cols) ? t.src[(int64_t)r * t.src_ld + c0 + k] : 0.f;
+  }
+  __syncthreads();
+  // output row j (= source column), 16 consecutive source rows
+  const int j = tid >> 2, i0 = (tid & 3) * 16;
+  TO* dst = base + t.dst_off + (int64_t)j * t.dst_ld + i0;
+  float v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = tile[i0 + k][j];
+  const bool vec = full && (t.dst_ld & 7) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+  if (vec) {
+    float a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { a[k] = v[k]; b[k] = v[8 + k]; }
+    reinterpret_cast<uint4*>(dst)[0] = pack_f<TO>(a);
+    reinterpret_cast<uint4*>(dst)[1] = pack_f<TO>(b);
+  } else if (j < t.cols) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (i0 + k < t.rows) dst[k] = from_f<TO>(v[k]);
+  }
+}
+}  // namespace
+
+extern "C" int mc_cast_transpose_f32_many(int32_t n_tiles, const mc_cast_t_tile* tiles, void* dst_base, int32_t dst_dtype,
+                                          void* stream) {
+  MC_CHECK(n_tiles >= 0 && (n_tiles == 0 || (tiles && dst_base)), MC_ERR_INVALID, "mc_cast_transpose_f32_many: bad tile table");
+  MC_CHECK(dst_dtype == MC_DTYPE_BF16 || dst_dtype == MC_DTYPE_F16, MC_ERR_DTYPE,
+           "mc_cast_transpose_f32_many: dst dtype %d (bf16 / f16 only)", dst_dtype);
+  if (n_tiles == 0) return MC_OK;
+  if (dst_dtype == MC_DTYPE_BF16)
+    hipLaunchKernelGGL(cast_transpose_kernel<bf16_t>, dim3(n_tiles), dim3(256), 0, (hipStream_t)stream, tiles,
+                       reinterpret_cast<bf16_t*>(dst_base));
+  else
+    hipLaunchKernelGGL(cast_transpose_kernel<f16_t>, dim3(n_tiles), dim3(256), 0, (hipStream_t)stream, tiles,
+                       reinterpret_cast<f16_t*>(dst_base));
+  return check_launch("mc_cast_transpose_f32_many");
+}
+
 // ---------------------------------------------------------------------------- split-K slab sums
 namespace {
 template <bool kVec>

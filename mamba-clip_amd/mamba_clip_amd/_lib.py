@@ -239,6 +239,7 @@ SYMBOLS = {
     "mc_qkv_grad_pack": (ctypes.c_int, [ctypes.POINTER(QkvPackParams), c_vp]),
     "mc_stream_copy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, c_vp]),
     "mc_cast_f32_many": (ctypes.c_int, [c_i32, c_vp, c_vp, c_i32, c_vp]),
+    "mc_cast_transpose_f32_many": (ctypes.c_int, [c_i32, c_vp, c_vp, c_i32, c_vp]),
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),

@@ -719,6 +719,8 @@ class GradHandoff:
 # a copy is never served for a later forward (parameters may have changed); the backward uses the
 # copies its forward saved, exactly as with per-use casts.
 _WCAST = None   # {id(param): (param, 16-bit copy)} while a scope is active
+_WCAST_T = None  # {id(param): (param, 16-bit TRANSPOSED copy)} for the weights _T_WANTED names
+_T_WANTED = set()   # ids of weights whose input gradient asked for a transposed copy (see _dgrad)
 _CAST_PLANS = {}
 
 
@@ -757,21 +759,63 @@ class _CastPlan:
         return [buf[o:o + p.numel()].view(p.shape) for o, p in zip(self.offs, params)]
 
 
+def _wcast_t(weight, x, dt):
+    """The 16-bit transposed copy of `weight` for the "tn" input gradient (_dgrad) when that form
+    applies to x @ weight^T, served from the active weight_cast_scope; None when the form does not
+    apply or the scope has no copy yet (the weight is then registered, and the next scope casts it)."""
+    if not (DGRAD_TN and WCAST_T and x.is_cuda and weight.dim() == 2 and weight.numel() >= 1 << 19
+            and x.numel() // max(x.shape[-1], 1) >= 8192):
+        return None
+    if _WCAST_T is not None:
+        e = _WCAST_T.get(id(weight))
+        if e is not None and e[0] is weight and e[1].dtype == dt:
+            return e[1]
+    if _WCAST is not None and weight.dtype == torch.float32:
+        _T_WANTED.add(id(weight))
+    return None
+
+
+class _TransposePlan:
+    """Tile table (device, mc_cast_t_tile = 4 x 8 B) and buffer layout for the transposed copies."""
+
+    def __init__(self, params, dt, device):
+        offs, off, rows = [], 0, []
+        for p in params:
+            R, C = p.shape
+            offs.append(off)
+            for r0 in range(0, R, 64):
+                for c0 in range(0, C, 64):
+                    rows.append((p.data_ptr() + 4 * (r0 * C + c0), off + c0 * R + r0,
+                                 C | (R << 32), min(64, R - r0) | (min(64, C - c0) << 32)))
+            off += (R * C + 7) // 8 * 8
+        self.offs, self.total, self.dt = offs, off, dt
+        self.ntiles = len(rows)
+        self.table = torch.tensor(rows, dtype=torch.int64).to(device)
+
+    def run(self, params):
+        buf = torch.empty(self.total, device=self.table.device, dtype=self.dt)
+        _lib.check(_lib.load().mc_cast_transpose_f32_many(self.ntiles, self.table.data_ptr(), buf.data_ptr(),
+                                                          _lib.dtype_code(self.dt), _lib.stream_handle(buf.device)),
+                   "mc_cast_transpose_f32_many")
+        return [buf[o:o + p.numel()].view(p.shape[1], p.shape[0]) for o, p in zip(self.offs, params)]
+
+
 class weight_cast_scope:
     """Context manager: one-launch 16-bit copies of `module`'s Linear weights / biases for one forward
     (no-op off the GPU, outside autocast, or when nested)."""
 
     def __init__(self, module, dt):
         self.module, self.dt, self.active = module, dt, False
-        self.buf = None
+        self.buf = self.buf_t = None
 
     def record_stream(self, stream):
         """The copies are used on another stream too (ClipModel's concurrent towers)."""
-        if self.buf is not None:
-            self.buf.record_stream(stream)
+        for b in (self.buf, self.buf_t):
+            if b is not None:
+                b.record_stream(stream)
 
     def __enter__(self):
-        global _WCAST
+        global _WCAST, _WCAST_T
         if _WCAST is not None or self.dt not in (torch.bfloat16, torch.float16):
             return self
         params = [p for m in self.module.modules() if isinstance(m, torch.nn.Linear)
@@ -787,25 +831,41 @@ class weight_cast_scope:
         copies = plan[1].run(params)
         self.buf = copies[0]
         _WCAST = {id(p): (p, c) for p, c in zip(params, copies)}
+        tparams = [p for p in params if p.dim() == 2 and id(p) in _T_WANTED]
+        if tparams:
+            tkey = (id(self.module), self.dt, "t", tuple((p.data_ptr(), p.shape) for p in tparams))
+            tplan = _CAST_PLANS.get(tkey[:3])
+            if tplan is None or tplan[0] != tkey:
+                tplan = (tkey, _TransposePlan(tparams, self.dt, params[0].device))
+                _CAST_PLANS[tkey[:3]] = tplan
+            tcopies = tplan[1].run(tparams)
+            self.buf_t = tcopies[0]
+            _WCAST_T = {id(p): (p, c) for p, c in zip(tparams, tcopies)}
         self.active = True
         return self
 
     def __exit__(self, *exc):
-        global _WCAST
+        global _WCAST, _WCAST_T
         if self.active:
-            _WCAST = None
+            _WCAST = _WCAST_T = None
         return False
 
 
 # Input gradients dx = g @ w of the towers' projections with the weight TRANSPOSED first: hipBLASLt
 # runs the "tn" form of these shapes (the forward's) faster than the "nn" form torch picks for a
 # row-major w -- e.g. the ViT fc2 input gradient (50432 x 3072 x 768): 0.246 ms nn vs 0.188 ms tn in
-# the tuning file (tuning/gemm_gfx950_dp.csv); a 16-bit transpose of w is ~5 us.  A/B toggle.
+# the tuning file (tuning/gemm_gfx950_dp.csv).  The transposed 16-bit copies come from the forward's
+# weight_cast_scope (mc_cast_transpose_f32_many, one launch for all of them: _wcast_t); a per-call
+# transpose of the 16-bit copy (~40 us each for the ViT's fc weights) is only the first step's
+# fallback.  A/B toggle.
 DGRAD_TN = os.environ.get("MAMBA_CLIP_AMD_DGRAD_TN", "1") != "0"
+WCAST_T = os.environ.get("MAMBA_CLIP_AMD_WCAST_T", "1") != "0"     # A/B: scope copies vs per-call transposes
 
 
-def _dgrad(g2, wc):
-    """g2 (M, N) @ wc (N, K) for a row-major weight copy wc."""
+def _dgrad(g2, wc, wt=None):
+    """g2 (M, N) @ wc (N, K) for a row-major weight copy wc (wt: its transposed copy, or None)."""
+    if wt is not None:
+        return torch.mm(g2, wt.t())
     if DGRAD_TN and g2.is_cuda and g2.shape[0] >= 8192 and wc.shape[0] * wc.shape[1] >= 1 << 19:
         return torch.mm(g2, wc.t().contiguous().t())
     return torch.mm(g2, wc)
@@ -829,6 +889,8 @@ class LinearSK(torch.autograd.Function):
             y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.has_bias = bias is not None
+        colmajor = xc.dim() == 2 and xc.stride(0) == 1 and xc.stride(1) != 1
+        ctx.wt = None if colmajor else _wcast_t(weight, xc, dt)
         return y
 
     @staticmethod
@@ -845,7 +907,7 @@ class LinearSK(torch.autograd.Function):
                 # backward needs no transpose copy
                 dx = torch.mm(wc.t(), g2.t()).t()
             else:
-                dx = _dgrad(g2, wc).view(xc.shape)
+                dx = _dgrad(g2, wc, ctx.wt).view(xc.shape)
         if ctx.needs_input_grad[1]:
             dw = wgrad(g2.t(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -1011,6 +1073,7 @@ class FC1GeluFn(torch.autograd.Function):
             h = torch.nn.functional.linear(xc, wc, bc)
             a = torch.nn.functional.gelu(h)
         ctx.save_for_backward(xc, wc, h)
+        ctx.wt = _wcast_t(weight, xc, dt)
         return a
 
     @staticmethod
@@ -1034,7 +1097,7 @@ class FC1GeluFn(torch.autograd.Function):
             gh = torch.ops.aten.gelu_backward(g2, h2)
             db = gh.sum(0, dtype=torch.float32)
         x2 = xc.reshape(-1, xc.shape[-1])
-        dx = _dgrad(gh, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(gh, wc, ctx.wt).view(xc.shape) if ctx.needs_input_grad[0] else None
         dw = wgrad(gh.t(), x2) if ctx.needs_input_grad[1] else None
         return dx, dw, db if ctx.needs_input_grad[2] else None
 
@@ -1059,6 +1122,7 @@ class QKVProjFn(torch.autograd.Function):
             y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.heads = heads
+        ctx.wt = _wcast_t(weight, xc, dt)
         q, k, v = y.view(Bsz, N, 3, heads, C // heads).unbind(2)
         return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
 
@@ -1093,7 +1157,7 @@ class QKVProjFn(torch.autograd.Function):
         else:   # CPU tensors (the CPU restatement tests): the same math in torch
             g2 = torch.stack([g.transpose(1, 2) for g in grads], dim=2).reshape(Bsz * N, 3 * C)
             db = g2.sum(0, dtype=torch.float32)
-        dx = _dgrad(g2, wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(g2, wc, ctx.wt).view(xc.shape) if ctx.needs_input_grad[0] else None
         dw = wgrad(g2.t(), xc.reshape(-1, C)) if ctx.needs_input_grad[1] else None
         return dx, dw, db if ctx.needs_input_grad[2] else None, None
 

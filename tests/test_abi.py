@@ -157,3 +157,18 @@ def test_cast_chunk_layout_matches_python_table():
         exe = os.path.join(d, "t")
         subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
         assert subprocess.check_output([exe]).decode().split() == ["24", "0", "8", "16"]
+
+
+def test_cast_transpose_tile_layout_matches_python_table():
+    """ops._TransposePlan packs each mc_cast_t_tile as four int64: src, dst_off, src_ld | dst_ld << 32,
+    rows | cols << 32 (little endian): the struct must be 32 B with fields at 0 / 8 / 16 / 20 / 24 / 28."""
+    f = ["src", "dst_off", "src_ld", "dst_ld", "rows", "cols"]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_ops.h"', "int main(void){",
+           'printf("%zu", sizeof(mc_cast_t_tile));'] + \
+          [f'printf(" %zu", offsetof(mc_cast_t_tile, {n}));' for n in f] + ['printf("\\n");', "return 0;}"]
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write("\n".join(src))
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
+        assert subprocess.check_output([exe]).decode().split() == ["32", "0", "8", "16", "20", "24", "28"]

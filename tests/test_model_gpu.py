@@ -725,6 +725,33 @@ def test_weight_cast_scope_bitwise_and_model_identical():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_weight_cast_scope_transposed_copies(dt):
+    """mc_cast_transpose_f32_many (the scope's transposed copies for the "tn" input gradients) gives
+    exactly w.to(dt).t() -- full 64 x 64 tiles, ragged edges and an odd leading dimension -- and a
+    LinearSK input gradient served from them is bitwise the per-call transpose's."""
+    import mamba_clip_amd.ops as O
+    torch.manual_seed(1)
+    ws = [torch.randn(r, c, device=DEV) for r, c in [(2304, 768), (768, 3072), (100, 70), (1, 5), (67, 129)]]
+    plan = O._TransposePlan(ws, dt, DEV)
+    for w, t in zip(ws, plan.run(ws)):
+        assert t.shape == (w.shape[1], w.shape[0]) and torch.equal(t, w.to(dt).t())
+    # the scope: the first forward registers, the next ones are served
+    lin = torch.nn.Linear(768, 3072).to(DEV)
+    x = torch.randn(8192 + 64, 768, device=DEV, dtype=dt)
+    g = torch.randn(8192 + 64, 3072, device=DEV, dtype=dt)
+    grads = []
+    for _ in range(3):
+        xx = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=dt), O.weight_cast_scope(lin, dt):
+            y = O.LinearSK.apply(xx, lin.weight, lin.bias)
+            served = O._WCAST_T is not None and id(lin.weight) in O._WCAST_T
+        y.backward(g)
+        grads.append((served, xx.grad.clone()))
+    assert [s for s, _ in grads] == [False, True, True]
+    assert torch.equal(grads[0][1], grads[1][1]) and torch.equal(grads[1][1], grads[2][1])
+
+
 @pytest.mark.parametrize("M,N,K", [(50432, 2304, 768), (20480, 80, 1536), (20480, 1536, 48), (16384, 37, 5)])
 def test_wgrad_split_k_slab_sum(M, N, K):
     """ops.wgrad (split-K strided-batched GEMM + mc_sum_slabs) against one fp32 GEMM of the same
