@@ -194,6 +194,12 @@ typedef struct mc_scan_bwd_params {
   int64_t dpx_batch_stride, dpx_token_stride, dpw_dim_stride;
   /* the interval the forward saved chunk_states with (0 = MC_SCAN_CHUNK) */
   int32_t state_interval;
+  /* Output strides of dB / dC (elements; seqlen stride 1).  All three 0: contiguous
+   * (batch, n_groups, dstate, seqlen).  A caller whose B / C are row blocks of one
+   * channel-major projection output (the Mamba mixer's x_proj rows) passes that
+   * block's strides, and the gradients land in the projection's gradient buffer. */
+  int64_t dB_batch_stride, dB_group_stride, dB_dstate_stride;
+  int64_t dC_batch_stride, dC_group_stride, dC_dstate_stride;
 } mc_scan_bwd_params;
 
 /* number of MC_SCAN_CHUNK-long chunks covering seqlen */

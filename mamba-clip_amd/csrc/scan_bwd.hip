@@ -56,6 +56,7 @@ struct BwdArgs {
   const float* chunk_states;
   void* du; void* ddelta; void* dz;
   float* slab_bc;                    // [b*G+g][nblk][seqlen][2][kN]  (dB partials, then dC partials)
+  int64_t bc_out_s[2][3];            // dB / dC output strides: batch, group, dstate (seqlen stride 1)
   float* slab_a;                     // [b][kN][dim] (dA partials, one owner per element)
   float* slab_d;                     // [b][dim]
   float* slab_bias;                  // [b][dim]
@@ -641,10 +642,13 @@ static hipError_t launch_bc_quads(const mc_scan_bwd_params* p, int np, f32x4* ou
 }
 
 // dB / dC: sum the per-workgroup slabs; dA / dD / dbias: sum the per-batch slabs.
+struct BcOutStrides {
+  int64_t s[2][3];
+};
 template <typename TW, int kN>
 __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, int G, int nblk,
                                                            int dstate, int L, int rev, TW* __restrict__ dB,
-                                                           TW* __restrict__ dC) {
+                                                           TW* __restrict__ dC, BcOutStrides os) {
   // thread -> (b*G+g, l, which, n), n fastest: the slab reads are coalesced
   const int64_t total = (int64_t)batch * G * L * 2 * kN;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -663,8 +667,10 @@ __global__ __launch_bounds__(256) void scan_bwd_reduce_bc(const float* __restric
 #pragma unroll 8
     for (int k = 0; k < nblk; ++k) s += sp[k * kst];
     TW* dst = which ? dC : dB;
-    const int lo = ((rev >> (int)(bgi % G)) & 1) ? L - 1 - l : l;
-    dst[(bgi * dstate + n) * L + lo] = from_f<TW>(s);
+    const int g = (int)(bgi % G);
+    const int lo = ((rev >> g) & 1) ? L - 1 - l : l;
+    const int64_t* st = os.s[which];
+    dst[(bgi / G) * st[0] + g * st[1] + n * st[2] + lo] = from_f<TW>(s);
   }
 }
 
@@ -785,7 +791,8 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL((scan_bwd_reduce_bc<TW, kN>), dim3(grid), dim3(256), 0, s, a.slab_bc, a.batch, a.n_groups,
                      a.nblk, a.dstate, a.seqlen, a.rev_groups, reinterpret_cast<TW*>(dB),
-                     reinterpret_cast<TW*>(dC));
+                     reinterpret_cast<TW*>(dC), BcOutStrides{{{a.bc_out_s[0][0], a.bc_out_s[0][1], a.bc_out_s[0][2]},
+                                                             {a.bc_out_s[1][0], a.bc_out_s[1][1], a.bc_out_s[1][2]}}});
   // slab_a is [b][n][d]: column c = n * dim + d -> dA[d][n] (transposed on output)
   const int ca = a.dim * a.dstate;
   hipLaunchKernelGGL(scan_bwd_colsum_nd, dim3((ca + 31) / 32), dim3(256), 0, s, a.slab_a, a.batch, a.dim, a.dstate,
@@ -798,8 +805,22 @@ static void launch_reduce(const BwdArgs& a, void* dB, void* dC, float* dA, float
                        nullptr, a.batch, a.dim, (int64_t)a.dim, dD ? dD : dbias, nullptr);
 }
 
+// dB / dC output strides from the params (all zero: contiguous (batch, G, dstate, seqlen))
+static void set_bc_out_strides(BwdArgs& a, const mc_scan_bwd_params* p) {
+  const int64_t ps[2][3] = {{p->dB_batch_stride, p->dB_group_stride, p->dB_dstate_stride},
+                            {p->dC_batch_stride, p->dC_group_stride, p->dC_dstate_stride}};
+  for (int w = 0; w < 2; ++w) {
+    const bool dflt = ps[w][0] == 0 && ps[w][1] == 0 && ps[w][2] == 0;
+    a.bc_out_s[w][0] = dflt ? (int64_t)a.n_groups * a.dstate * a.seqlen : ps[w][0];
+    a.bc_out_s[w][1] = dflt ? (int64_t)a.dstate * a.seqlen : ps[w][1];
+    a.bc_out_s[w][2] = dflt ? (int64_t)a.seqlen : ps[w][2];
+  }
+}
+
 template <typename TW>
-static void launch_reduce_t(const BwdArgs& a, void* dB, void* dC, float* dA, float* dD, float* dbias, hipStream_t s) {
+static void launch_reduce_t(BwdArgs& a, const mc_scan_bwd_params* p, void* dB, void* dC, float* dA, float* dD,
+                            float* dbias, hipStream_t s) {
+  set_bc_out_strides(a, p);
   const int np = padded_dstate(a.dstate);
   if (np == 8) launch_reduce<TW, 8>(a, dB, dC, dA, dD, dbias, s);
   else if (np == 16) launch_reduce<TW, 16>(a, dB, dC, dA, dD, dbias, s);
@@ -900,9 +921,9 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
     launch_bwd_pair(p, a.slab_bc, a.slab_a, a.slab_d, a.slab_bias, a.nblk, s);
     e = hipGetLastError();
     MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: launch failed: %s", hipGetErrorString(e));
-    if (p->wtype == MC_DTYPE_F32) launch_reduce_t<float>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
-    else if (p->wtype == MC_DTYPE_BF16) launch_reduce_t<bf16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
-    else launch_reduce_t<f16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    if (p->wtype == MC_DTYPE_F32) launch_reduce_t<float>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    else if (p->wtype == MC_DTYPE_BF16) launch_reduce_t<bf16_t>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+    else launch_reduce_t<f16_t>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
     e = hipGetLastError();
     MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: reduce launch failed: %s", hipGetErrorString(e));
     return MC_OK;
@@ -959,9 +980,9 @@ extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   else if (p->itype == MC_DTYPE_BF16) rc = launch_bwd_t<bf16_t>(a, aligned, s);
   else rc = launch_bwd_t<f16_t>(a, aligned, s);
   if (rc) return rc;
-  if (p->wtype == MC_DTYPE_F32) launch_reduce_t<float>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
-  else if (p->wtype == MC_DTYPE_BF16) launch_reduce_t<bf16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
-  else launch_reduce_t<f16_t>(a, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+  if (p->wtype == MC_DTYPE_F32) launch_reduce_t<float>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+  else if (p->wtype == MC_DTYPE_BF16) launch_reduce_t<bf16_t>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
+  else launch_reduce_t<f16_t>(a, p, p->dB, p->dC, p->dA, p->dD, p->ddelta_bias, s);
   e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_scan_bwd: reduce launch failed: %s", hipGetErrorString(e));
   return MC_OK;

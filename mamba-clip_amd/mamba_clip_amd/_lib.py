@@ -68,6 +68,8 @@ class ScanBwdParams(ctypes.Structure):
         ("delta_proj_x", c_vp), ("delta_proj_w", c_vp), ("delta_rank", c_i32),
         ("dpx_batch_stride", c_i64), ("dpx_token_stride", c_i64), ("dpw_dim_stride", c_i64),
         ("state_interval", c_i32),
+        ("dB_batch_stride", c_i64), ("dB_group_stride", c_i64), ("dB_dstate_stride", c_i64),
+        ("dC_batch_stride", c_i64), ("dC_group_stride", c_i64), ("dC_dstate_stride", c_i64),
     ]
 
 

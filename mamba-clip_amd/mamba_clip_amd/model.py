@@ -33,6 +33,7 @@ import torch.utils.checkpoint
 from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
                   fc1_gelu, linear_sk, mixer_proj, mixer_proj_ok, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
+                  split_rows_n,
                   ss2d_conv_stack, ss2d_merge_ln_gate, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
@@ -46,10 +47,14 @@ def _dt_bias_init(d_inner, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
     return dt + torch.log(-torch.expm1(-dt))
 
 
-def mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None):
+XPROJ_GRAD_SLAB = os.environ.get("MAMBA_CLIP_AMD_XPROJ_GRAD_SLAB", "1") != "0"   # A/B toggle
+
+
+def mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None, dbc_slab=None):
     """The mixer's scan call (selective_scan_fn semantics, softplus on) with dz written into
-    the in_proj gradient slab and du handed to x_proj's backward (ops.GradHandoff)."""
-    return SelectiveScanFn.apply(x, delta, A, Bm, Cm, D, z, delta_bias, True, False, dz_slab, du_handoff)
+    the in_proj gradient slab, dB / dC into the x_proj gradient slab and du handed to x_proj's
+    backward (ops.GradHandoff)."""
+    return SelectiveScanFn.apply(x, delta, A, Bm, Cm, D, z, delta_bias, True, False, dz_slab, du_handoff, dbc_slab)
 
 
 class MambaMixer(nn.Module):
@@ -131,11 +136,17 @@ class MambaMixer(nn.Module):
             # GEMM epilogue (ops.GradHandoff) instead of autograd summing the two producers
             hand = GradHandoff() if (self.du_handoff and x.is_cuda and x.requires_grad) else None
             x_dbl = wleft_mm(self.x_proj.weight, x_cm, hand)                   # (R+2N, B*L)
-            dt_raw, Bm, Cm = x_dbl.split([R, N, N], dim=0)
-            delta = wleft_mm(self.dt_proj.weight, dt_raw).view(di, Bsz, L).transpose(0, 1)
+            # dt_proj's backward writes d(dt_raw) and the scan's writes dB / dC straight into one
+            # (R+2N, B*L) gradient slab: no transpose copies of dB / dC, no concatenation
+            pslab = GradSlab(R + 2 * N, Bsz * L, x_dbl.dtype, x_dbl.device) if (x_dbl.requires_grad and
+                                                                                 XPROJ_GRAD_SLAB) else None
+            dt_raw, Bm, Cm = split_rows_n(x_dbl, (R, N, N), pslab)
+            delta = wleft_mm(self.dt_proj.weight, dt_raw, out_slab=(pslab, 0) if pslab is not None else None)
+            delta = delta.view(di, Bsz, L).transpose(0, 1)
             Bm = Bm.view(N, Bsz, L).transpose(0, 1)                           # (B, N, L)
             Cm = Cm.view(N, Bsz, L).transpose(0, 1)
-            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz, hand)
+            y = mixer_scan(x, delta, A, Bm, Cm, self.D.float(), z, self.dt_proj.bias.float(), dz, hand,
+                           (pslab, R, R + N) if pslab is not None else None)
         y2 = y.transpose(0, 1).reshape(di, Bsz * L)                            # view: y keeps x's layout
         out = linear_sk(y2.t(), self.out_proj.weight)                          # (B*L, d_model)
         return out.view(Bsz, L, dm)

@@ -495,6 +495,39 @@ def split_rows(X, k, slab=None):
     return SplitRowsFn.apply(X, k, slab)
 
 
+class SplitRowsNFn(torch.autograd.Function):
+    """Row blocks of `sizes` of a 2-D activation (the mixer's x_proj output: dt_raw, B, C rows);
+    backward returns the slab when every block's gradient already lives in it, else concatenates."""
+
+    @staticmethod
+    def forward(ctx, X, sizes, slab):
+        ctx.sizes, ctx.slab, ctx.shape = sizes, slab, X.shape
+        return X.split(list(sizes), dim=0)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        slab, sizes = ctx.slab, ctx.sizes
+        buf = slab.buf if slab is not None else None
+        if buf is not None and all(g is not None for g in grads):
+            r0, ok = 0, True
+            for g, n in zip(grads, sizes):
+                blk = buf[r0:r0 + n]
+                ok = ok and g.data_ptr() == blk.data_ptr() and g.shape == blk.shape and g.stride() == blk.stride()
+                r0 += n
+            if ok:
+                slab.shared = True
+                return buf, None, None
+        cols = ctx.shape[1]
+        ref = next(g for g in grads if g is not None)
+        parts = [g.reshape(n, cols) if g is not None else torch.zeros(n, cols, dtype=ref.dtype, device=ref.device)
+                 for g, n in zip(grads, sizes)]
+        return torch.cat(parts), None, None
+
+
+def split_rows_n(X, sizes, slab=None):
+    return SplitRowsNFn.apply(X, tuple(sizes), slab)
+
+
 class CausalConv1dFn(torch.autograd.Function):
     """Depthwise causal conv1d (+SiLU) over (batch, dim, seqlen); output contiguous."""
 
@@ -927,13 +960,14 @@ class WeightLeftMM(torch.autograd.Function):
     """y = w @ X for a weight w (N, K) and activations X (K, M) (channel-major GEMMs of the Mamba mixer)."""
 
     @staticmethod
-    def forward(ctx, weight, X, handoff=None):
+    def forward(ctx, weight, X, handoff=None, out_slab=None):
         dt = _compute_dtype(X)
         wc, Xc = _wcast(weight, dt), X.to(dt)
         with torch.autocast("cuda", enabled=False):
             y = torch.mm(wc, Xc)
         ctx.save_for_backward(wc, Xc)
         ctx.handoff = handoff
+        ctx.out_slab = out_slab   # (GradSlab, first row): dX written into those rows (ops.GradSlab)
         return y
 
     @staticmethod
@@ -955,15 +989,19 @@ class WeightLeftMM(torch.autograd.Function):
                 acc = None
             elif Xc.stride(0) == 1 and Xc.stride(1) != 1:
                 dX = torch.mm(g.t(), wc).t()      # X is a transposed view: keep its layout (no copy downstream)
+            elif ctx.out_slab is not None and acc is None and Xc.is_contiguous():
+                slab, r0 = ctx.out_slab
+                dX = slab.get()[r0:r0 + Xc.shape[0]]
+                torch.mm(wc.t(), g, out=dX)
             else:
                 dX = torch.mm(wc.t(), g)
             if acc is not None:   # handed-off gradient in another layout: summed after the GEMM
                 dX = dX + acc.transpose(0, 1).reshape(Xc.shape)
-        return dw, dX, None
+        return dw, dX, None, None
 
 
-def wleft_mm(weight, X, handoff=None):
-    return WeightLeftMM.apply(weight, X, handoff)
+def wleft_mm(weight, X, handoff=None, out_slab=None):
+    return WeightLeftMM.apply(weight, X, handoff, out_slab)
 
 
 def mixer_proj_ok(x_cm, rank, dstate):

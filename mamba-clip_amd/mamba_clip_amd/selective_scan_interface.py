@@ -155,9 +155,11 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     return out, states, last
 
 
-def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None, proj=None):
+def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None, proj=None,
+             dbc_out=None):
     """Run mc_scan_bwd.  With ``dirs``, du comes back per group, (B, dim, L): the caller sums the
-    groups that share a u block.  ``proj=(dpx, dpw)``: projected delta (delta None), as scan_fwd."""
+    groups that share a u block.  ``proj=(dpx, dpw)``: projected delta (delta None), as scan_fwd.
+    ``dbc_out=(dB, dC)``: (batch, G, dstate, L) views (seqlen stride 1) the gradients are written into."""
     lib = _lib.load()
     if delta is None:
         delta = u   # shape / layout template only: with proj the kernel re-forms delta, never reads it
@@ -168,8 +170,14 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
     du = torch.empty_like(u) if dirs is None else torch.empty_like(delta)
     ddelta = torch.empty_like(delta)
     dz = (dz_out if dz_out is not None else torch.empty_like(z)) if z is not None else None
-    dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
-    dC = torch.empty(C.shape, device=u.device, dtype=C.dtype)
+    if dbc_out is not None:
+        dB, dC = dbc_out
+        if dB.shape != B.shape or dC.shape != C.shape or dB.dtype != B.dtype or dC.dtype != C.dtype \
+                or dB.stride(-1) != 1 or dC.stride(-1) != 1:
+            raise ValueError("scan_bwd: dbc_out views must match B / C (shape, dtype, seqlen stride 1)")
+    else:
+        dB = torch.empty(B.shape, device=u.device, dtype=B.dtype)
+        dC = torch.empty(C.shape, device=u.device, dtype=C.dtype)
     dA = torch.empty(dim, dstate, device=u.device, dtype=torch.float32)
     dD = torch.empty(dim, device=u.device, dtype=torch.float32) if D is not None else None
     dbias = torch.empty(dim, device=u.device, dtype=torch.float32) if delta_bias is not None else None
@@ -200,6 +208,9 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
         p.delta_proj_x, p.delta_proj_w, p.delta_rank = dpx.data_ptr(), dpw.data_ptr(), dpw.shape[1]
         p.dpx_batch_stride, p.dpx_token_stride, p.dpw_dim_stride = dpx.stride(0), dpx.stride(1), dpw.stride(0)
     p.du, p.ddelta, p.dz, p.dB, p.dC = du.data_ptr(), ddelta.data_ptr(), _lib.ptr(dz), dB.data_ptr(), dC.data_ptr()
+    if dbc_out is not None:
+        p.dB_batch_stride, p.dB_group_stride, p.dB_dstate_stride = dB.stride(0), dB.stride(1), dB.stride(2)
+        p.dC_batch_stride, p.dC_group_stride, p.dC_dstate_stride = dC.stride(0), dC.stride(1), dC.stride(2)
     p.dA, p.dD, p.ddelta_bias = dA.data_ptr(), _lib.ptr(dD), _lib.ptr(dbias)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
     if dirs is not None:
@@ -213,7 +224,7 @@ class SelectiveScanFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
-                return_last_state=False, dz_slab=None, du_handoff=None):
+                return_last_state=False, dz_slab=None, du_handoff=None, dbc_slab=None):
         u, delta, z = _last_dim_contig(u), _last_dim_contig(delta), _last_dim_contig(z)
         squeeze_B, squeeze_C = B.dim() == 3, C.dim() == 3
         B, C = _prep_bc(B, "B"), _prep_bc(C, "C")
@@ -233,6 +244,7 @@ class SelectiveScanFn(torch.autograd.Function):
         ctx.has = (D is not None, z is not None, delta_bias is not None)
         ctx.dz_slab = dz_slab   # (GradSlab, first row): dz written into that slab (ops.GradSlab)
         ctx.du_handoff = du_handoff   # ops.GradHandoff: du parked for x_proj's backward (no u gradient here)
+        ctx.dbc_slab = dbc_slab       # (GradSlab, B's first row, C's first row): dB / dC written there
         return (out, last) if return_last_state else out
 
     @staticmethod
@@ -242,8 +254,14 @@ class SelectiveScanFn(torch.autograd.Function):
         if ctx.dz_slab is not None and z is not None:
             slab, r0 = ctx.dz_slab
             dz_out = slab.block(r0, r0 + z.shape[1], z.shape[0])
+        dbc_out = None
+        if ctx.dbc_slab is not None and B.shape[1] == 1 and C.shape[1] == 1:
+            slab, rb, rc = ctx.dbc_slab
+            n, bsz = B.shape[2], B.shape[0]
+            dbc_out = (slab.block(rb, rb + n, bsz).unsqueeze(1), slab.block(rc, rc + n, bsz).unsqueeze(1))
         du, ddelta, dA, dB, dC, dD, dz, dbias = scan_bwd(u, delta, A32, B, C, D32, z, bias32,
-                                                         ctx.delta_softplus, dout, states, dz_out=dz_out)
+                                                         ctx.delta_softplus, dout, states, dz_out=dz_out,
+                                                         dbc_out=dbc_out)
         if ctx.squeeze[0]:
             dB = dB.squeeze(1)
         if ctx.squeeze[1]:
@@ -255,7 +273,7 @@ class SelectiveScanFn(torch.autograd.Function):
                 dD.to(d_dt) if dD is not None else None,
                 dz,
                 dbias.to(b_dt) if dbias is not None else None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 class ProjectedScanFn(torch.autograd.Function):

@@ -100,7 +100,7 @@ def ss2d_merge_ln_gate_ref(out, z, ln_weight, ln_bias, eps):
     return F.layer_norm(y, (C,), ln_weight, ln_bias, eps) * F.silu(z)
 
 
-def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None):
+def _mixer_scan(x, delta, A, Bm, Cm, D, z, delta_bias, dz_slab, du_handoff=None, dbc_slab=None):
     return selective_scan_ref(x, delta, A, Bm, Cm, D, z=z, delta_bias=delta_bias, delta_softplus=True)
 
 

@@ -302,14 +302,28 @@ def test_mamba_mixer_matches_oracle():
     torch.testing.assert_close(h.grad.cpu().double(), hr.grad, rtol=1e-3, atol=1e-4)
 
 
-def test_mamba_mixer_xz_gradient_slab_no_concat():
-    """The conv / scan backward kernels write dx / dz into one slab: the in_proj split's gradient
-    is that slab (no concatenation), with the same in_proj weight gradient as the copying path."""
+@pytest.mark.parametrize("amp", [False, True])
+def test_mamba_mixer_gradient_slabs_no_concat(amp):
+    """The conv / scan backward kernels write dx / dz into one slab (the in_proj split's gradient),
+    and dt_proj's backward GEMM plus the scan's dB / dC reduction write into another (the x_proj
+    split's gradient): no transpose copies or concatenation, and every gradient bitwise the same as
+    the copying path.  amp: bf16 autocast at a C2-like width (the lane-pair scan kernels)."""
     from mamba_clip_amd import ops
     from mamba_clip_amd.model import MambaMixer
+    import mamba_clip_amd.model as M
     torch.manual_seed(1)
-    m = MambaMixer(64, d_state=16).to(DEV)
-    h = torch.randn(3, 48, 64, device=DEV, requires_grad=True)
+    d = 256 if amp else 64
+    m = MambaMixer(d, d_state=16).to(DEV)
+    h = torch.randn(3, 48, d, device=DEV, requires_grad=True)
+
+    def run():
+        m.zero_grad()
+        h.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = m(h)
+        y.float().square().sum().backward()
+        return [h.grad.clone()] + [p.grad.clone() for p in m.parameters()]
+
     made = []
     orig = ops.GradSlab.__init__
 
@@ -319,23 +333,18 @@ def test_mamba_mixer_xz_gradient_slab_no_concat():
 
     ops.GradSlab.__init__ = spy
     try:
-        m(h).square().sum().backward()
+        with_slab = run()
     finally:
         ops.GradSlab.__init__ = orig
-    assert len(made) == 1 and getattr(made[0], "shared", False)
-    g_slab, gh_slab = m.in_proj.weight.grad.clone(), h.grad.clone()
-    # the same step with the slab disabled (plain concatenation)
-    m.zero_grad()
-    h.grad = None
-    import mamba_clip_amd.model as M
+    assert len(made) == 2 and all(getattr(s, "shared", False) for s in made)
     real = M.GradSlab
-    M.GradSlab = lambda *a, **k: None
+    M.GradSlab = lambda *a, **k: None     # the same step with plain concatenation
     try:
-        m(h).square().sum().backward()
+        plain = run()
     finally:
         M.GradSlab = real
-    torch.testing.assert_close(m.in_proj.weight.grad, g_slab, rtol=0, atol=0)
-    torch.testing.assert_close(h.grad, gh_slab, rtol=0, atol=0)
+    for a, b in zip(with_slab, plain):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
