@@ -2,7 +2,7 @@
 # Round-4 final measurements: default bench (C2 + roofline + CPU baseline), its rocprof kernel stats,
 # C3 bench, C4 scan backward rocprof + PMC, scan-forward PMC traffic.  Each step under its own limit.
 set -u
-out=gpurun_out/r04final; mkdir -p $out
+out=gpurun_out/${R04_OUT:-r04final}; mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python bench.py > $out/bench_c2_n1.json 2> $out/bench_c2_n1.err || { echo bench failed; tail -20 $out/bench_c2_n1.err; exit 2; }
 cat $out/bench_c2_n1.json
