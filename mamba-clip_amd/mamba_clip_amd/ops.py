@@ -14,6 +14,7 @@ All launches go on the current HIP stream; nothing synchronises.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -753,7 +754,7 @@ class GradHandoff:
 # copies its forward saved, exactly as with per-use casts.
 _WCAST = None   # {id(param): (param, 16-bit copy)} while a scope is active
 _WCAST_T = None  # {id(param): (param, 16-bit TRANSPOSED copy)} for the weights _T_WANTED names
-_T_WANTED = set()   # ids of weights whose input gradient asked for a transposed copy (see _dgrad)
+_T_WANTED = weakref.WeakValueDictionary()   # id -> weight whose input gradient asked for a transposed copy
 _CAST_PLANS = {}
 
 
@@ -804,7 +805,7 @@ def _wcast_t(weight, x, dt):
         if e is not None and e[0] is weight and e[1].dtype == dt:
             return e[1]
     if _WCAST is not None and weight.dtype == torch.float32:
-        _T_WANTED.add(id(weight))
+        _T_WANTED[id(weight)] = weight
     return None
 
 
@@ -864,7 +865,7 @@ class weight_cast_scope:
         copies = plan[1].run(params)
         self.buf = copies[0]
         _WCAST = {id(p): (p, c) for p, c in zip(params, copies)}
-        tparams = [p for p in params if p.dim() == 2 and id(p) in _T_WANTED]
+        tparams = [p for p in params if p.dim() == 2 and _T_WANTED.get(id(p)) is p]
         if tparams:
             tkey = (id(self.module), self.dt, "t", tuple((p.data_ptr(), p.shape) for p in tparams))
             tplan = _CAST_PLANS.get(tkey[:3])
