@@ -167,6 +167,36 @@ typedef struct mc_cast_t_tile {
 int mc_cast_transpose_f32_many(int32_t n_tiles, const mc_cast_t_tile* tiles, void* dst_base, int32_t dst_dtype,
                                void* stream);
 
+/* AdamW step over many fp32 parameters in one launch (replaces torch.optim.AdamW's step in the
+ * reference's train loop, train.py:183-198 / create_optimizer; decoupled weight decay, no amsgrad):
+ *   p *= 1 - lr * wd;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;
+ *   p -= step_size * m / (sqrt(v) / bc2_sqrt + eps),  step_size = lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t).
+ * tensors: DEVICE array, one entry per parameter (g may change every step); chunks: DEVICE array,
+ * one entry per <= MC_ADAMW_CHUNK elements of a tensor (off a multiple of 4); hyper: host struct,
+ * passed by value to the kernel (hyper-parameters and bias corrections of this step, per group). */
+#define MC_ADAMW_MAX_GROUPS 8
+#define MC_ADAMW_CHUNK 65536
+typedef struct mc_adamw_tensor {
+  float* p;
+  float* m;
+  float* v;
+  const float* g;
+} mc_adamw_tensor;
+typedef struct mc_adamw_chunk {
+  int32_t tensor, group;
+  int64_t off, n;
+} mc_adamw_chunk;
+typedef struct mc_adamw_group {
+  float beta1, beta2, eps, decay;    /* decay = 1 - lr * weight_decay */
+  float step_size, bc2_sqrt;
+} mc_adamw_group;
+typedef struct mc_adamw_hyper {
+  int32_t n_groups, reserved;
+  mc_adamw_group group[MC_ADAMW_MAX_GROUPS];
+} mc_adamw_hyper;
+int mc_adamw_step(int32_t n_chunks, const mc_adamw_chunk* chunks, const mc_adamw_tensor* tensors,
+                  const mc_adamw_hyper* hyper, void* stream);
+
 /* ---- Mamba mixer projections (mixer_proj.hip): x_proj and dt_proj around the scan, fused.
  * Reference: the mixer's x_dbl = x_proj(x), delta = dt_proj.weight @ dt_raw (upstream
  * mamba_simple.Mamba; SS2D's analogue model.py:519-528, 630-647).  Channel-major activations

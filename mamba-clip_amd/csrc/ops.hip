@@ -1283,6 +1283,61 @@ extern "C" int mc_cast_transpose_f32_many(int32_t n_tiles, const mc_cast_t_tile*
   return check_launch("mc_cast_transpose_f32_many");
 }
 
+// ---------------------------------------------------------------------------- AdamW over many tensors
+namespace {
+__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, const mc_adamw_group& h) {
+  p *= h.decay;
+  m = h.beta1 * m + (1.f - h.beta1) * g;
+  v = h.beta2 * v + (1.f - h.beta2) * g * g;
+  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
+  p -= h.step_size * m / denom;
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(const mc_adamw_chunk* __restrict__ chunks,
+                                                    const mc_adamw_tensor* __restrict__ tensors, const mc_adamw_hyper hy) {
+  const mc_adamw_chunk c = chunks[blockIdx.x];
+  const mc_adamw_tensor t = tensors[c.tensor];
+  const mc_adamw_group h = hy.group[c.group];
+  float* __restrict__ p = t.p + c.off;
+  float* __restrict__ m = t.m + c.off;
+  float* __restrict__ v = t.v + c.off;
+  const float* __restrict__ g = t.g + c.off;
+  const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v) |
+                     reinterpret_cast<uintptr_t>(g)) & 15) == 0;
+  const int64_t n4 = vec ? c.n / 4 : 0;
+  for (int64_t i = threadIdx.x; i < n4; i += 256) {
+    float4 pp = reinterpret_cast<float4*>(p)[i], mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    adamw_elem(pp.x, mm.x, vv.x, gg.x, h);
+    adamw_elem(pp.y, mm.y, vv.y, gg.y, h);
+    adamw_elem(pp.z, mm.z, vv.z, gg.z, h);
+    adamw_elem(pp.w, mm.w, vv.w, gg.w, h);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (int64_t i = 4 * n4 + threadIdx.x; i < c.n; i += 256) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adamw_elem(pp, mm, vv, g[i], h);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+}  // namespace
+
+extern "C" int mc_adamw_step(int32_t n_chunks, const mc_adamw_chunk* chunks, const mc_adamw_tensor* tensors,
+                             const mc_adamw_hyper* hyper, void* stream) {
+  MC_CHECK(n_chunks >= 0 && hyper, MC_ERR_INVALID, "mc_adamw_step: bad arguments");
+  MC_CHECK(hyper->n_groups >= 1 && hyper->n_groups <= MC_ADAMW_MAX_GROUPS, MC_ERR_INVALID,
+           "mc_adamw_step: n_groups %d (1..%d)", hyper->n_groups, MC_ADAMW_MAX_GROUPS);
+  if (n_chunks == 0) return MC_OK;
+  MC_CHECK(chunks && tensors, MC_ERR_INVALID, "mc_adamw_step: null chunk / tensor table");
+  hipLaunchKernelGGL(adamw_kernel, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, chunks, tensors, *hyper);
+  return check_launch("mc_adamw_step");
+}
+
 // ---------------------------------------------------------------------------- split-K slab sums
 namespace {
 template <bool kVec>

@@ -73,6 +73,21 @@ class ScanBwdParams(ctypes.Structure):
     ]
 
 
+MC_ADAMW_MAX_GROUPS = 8
+MC_ADAMW_CHUNK = 65536
+
+
+class AdamWGroup(ctypes.Structure):
+    """Mirror of ``mc_adamw_group`` (include/mc_ops.h)."""
+    _fields_ = [("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("decay", ctypes.c_float),
+                ("step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float)]
+
+
+class AdamWHyper(ctypes.Structure):
+    """Mirror of ``mc_adamw_hyper`` (include/mc_ops.h)."""
+    _fields_ = [("n_groups", ctypes.c_int32), ("reserved", ctypes.c_int32), ("group", AdamWGroup * MC_ADAMW_MAX_GROUPS)]
+
+
 class MixerProjParams(ctypes.Structure):
     """Mirror of ``mc_mixer_proj_params`` (include/mc_ops.h)."""
     _fields_ = [
@@ -242,6 +257,7 @@ SYMBOLS = {
     "mc_stream_copy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, c_vp]),
     "mc_cast_f32_many": (ctypes.c_int, [c_i32, c_vp, c_vp, c_i32, c_vp]),
     "mc_cast_transpose_f32_many": (ctypes.c_int, [c_i32, c_vp, c_vp, c_i32, c_vp]),
+    "mc_adamw_step": (ctypes.c_int, [c_i32, c_vp, c_vp, ctypes.POINTER(AdamWHyper), c_vp]),
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnFwdParams), c_vp]),
     "mc_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnBwdParams), c_vp]),

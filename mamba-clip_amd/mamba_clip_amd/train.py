@@ -19,6 +19,7 @@ inputs, so the loss sees the original targets (train.py:66-89, 189).
 """
 import logging
 import math
+import os
 import time
 
 import numpy as np
@@ -26,6 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from .data import normalize_images
+from .optim import HipAdamW
 from .utils.amp_utils import get_autocast, get_input_dtype
 from .utils.dist_utils import is_master
 
@@ -81,6 +83,9 @@ def _no_decay(name, p):
     return p.ndim < 2 or "bn" in name or "ln" in name or "bias" in name or "logit_scale" in name
 
 
+HIP_ADAMW = os.environ.get("MAMBA_CLIP_AMD_HIP_ADAMW", "1") != "0"   # A/B toggle (torch fused AdamW when 0)
+
+
 def create_optimizer(model, args):
     """AdamW with two groups: gains/biases/logit_scale at wd 0, the rest at args.wd.
 
@@ -91,10 +96,14 @@ def create_optimizer(model, args):
     groups = [{"params": [p for n, p in named if _no_decay(n, p)], "weight_decay": 0.0},
               {"params": [p for n, p in named if not _no_decay(n, p)], "weight_decay": args.wd}]
     on_gpu = all(p.is_cuda for _, p in named)
+    capturable = bool(on_gpu and getattr(args, "capturable", False))
+    if on_gpu and not capturable and HIP_ADAMW and all(p.dtype == torch.float32 for _, p in named):
+        # one HIP launch over every parameter (optim.HipAdamW, mc_adamw_step): same rule and state layout
+        return HipAdamW(groups, lr=args.lr, betas=(args.beta1, args.beta2), eps=args.eps)
     # capturable: the step counts live on the device, so a HIP-graph replay (GraphedStep) advances them
     return torch.optim.AdamW(groups, lr=args.lr, betas=(args.beta1, args.beta2), eps=args.eps,
                              fused=True if on_gpu else None,
-                             capturable=bool(on_gpu and getattr(args, "capturable", False)))
+                             capturable=capturable)
 
 
 def create_scaler(args, device):
