@@ -172,3 +172,24 @@ def test_cast_transpose_tile_layout_matches_python_table():
         exe = os.path.join(d, "t")
         subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
         assert subprocess.check_output([exe]).decode().split() == ["32", "0", "8", "16", "20", "24", "28"]
+
+
+def test_adamw_tables_match_python_layout():
+    """optim.HipAdamW packs mc_adamw_chunk as int64 (tensor | group << 32, off, n) and mc_adamw_tensor as
+    four pointers; _lib.AdamWHyper mirrors mc_adamw_hyper (passed by pointer, read by value)."""
+    from mamba_clip_amd import _lib
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_ops.h"', "int main(void){",
+           'printf("%zu %zu %zu %zu %zu ", sizeof(mc_adamw_chunk), offsetof(mc_adamw_chunk, tensor), '
+           'offsetof(mc_adamw_chunk, group), offsetof(mc_adamw_chunk, off), offsetof(mc_adamw_chunk, n));',
+           'printf("%zu %zu ", sizeof(mc_adamw_tensor), offsetof(mc_adamw_tensor, g));',
+           'printf("%zu %zu %zu\\n", sizeof(mc_adamw_hyper), offsetof(mc_adamw_hyper, group), sizeof(mc_adamw_group));',
+           "return 0;}"]
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write("\n".join(src))
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", INCLUDE, c, "-o", exe])
+        got = [int(x) for x in subprocess.check_output([exe]).decode().split()]
+    assert got[:5] == [24, 0, 4, 8, 16] and got[5:7] == [32, 24]
+    assert got[7] == ctypes.sizeof(_lib.AdamWHyper) and got[8] == _lib.AdamWHyper.group.offset
+    assert got[9] == ctypes.sizeof(_lib.AdamWGroup)
