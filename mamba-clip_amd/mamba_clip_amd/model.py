@@ -426,7 +426,7 @@ class ClipModel(nn.Module):
     concurrent_towers = os.environ.get("MAMBA_CLIP_AMD_CONCURRENT_TOWERS", "1") != "0"
     ddp_streams_joined = False
     last_main_stream = None
-    side_high_priority = False   # text-tower stream at HIP's high priority (A/B toggle)
+    side_high_priority = os.environ.get("MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY", "0") == "1"   # text-tower stream priority (A/B)
     _side_streams = {}
 
     def side_stream_for(self, device):
