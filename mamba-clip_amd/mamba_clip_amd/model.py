@@ -426,8 +426,17 @@ class ClipModel(nn.Module):
     concurrent_towers = os.environ.get("MAMBA_CLIP_AMD_CONCURRENT_TOWERS", "1") != "0"
     ddp_streams_joined = False
     last_main_stream = None
-    side_high_priority = os.environ.get("MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY", "0") == "1"   # text-tower stream priority (A/B)
     _side_streams = {}
+
+    @property
+    def side_high_priority(self):
+        """Text-tower stream at HIP's high priority: on beside the BERT tower (C3 25.3 -> 25.0 ms per
+        step), off beside the Mamba tower (C2 69.9 -> 70.8 ms with it); profiles/r04/stream_priority/.
+        MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY=0/1 overrides (A/B)."""
+        env = os.environ.get("MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY")
+        if env is not None:
+            return env == "1"
+        return isinstance(self.text, BertTextEncoder)
 
     def side_stream_for(self, device):
         device = torch.device(device)
