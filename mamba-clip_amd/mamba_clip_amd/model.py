@@ -429,22 +429,36 @@ class ClipModel(nn.Module):
     _side_streams = {}
 
     @property
-    def side_high_priority(self):
-        """Text-tower stream at HIP's high priority: on beside the BERT tower (C3 25.3 -> 25.0 ms per
-        step), off beside the Mamba tower (C2 69.9 -> 70.8 ms with it); profiles/r04/stream_priority/.
-        MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY=0/1 overrides (A/B)."""
-        env = os.environ.get("MAMBA_CLIP_AMD_SIDE_HIGH_PRIORITY")
+    def side_priority(self):
+        """HIP priority of the text-tower stream (-1 high, 0 normal, 1 low where the device has it):
+        high beside the BERT tower (C3 25.3 -> 25.0 ms per step), normal beside the Mamba tower
+        (C2 69.9 -> 70.8 ms at high); profiles/r04/stream_priority/.  MAMBA_CLIP_AMD_SIDE_PRIORITY
+        overrides (A/B)."""
+        env = os.environ.get("MAMBA_CLIP_AMD_SIDE_PRIORITY")
         if env is not None:
-            return env == "1"
-        return isinstance(self.text, BertTextEncoder)
+            return int(env)
+        return -1 if isinstance(self.text, BertTextEncoder) else 0
+
+    @property
+    def side_tower(self):
+        """Which tower runs on the side stream: the image tower beside the Mamba text tower (C2 69.2 ->
+        68.9 ms per step), the text tower beside BERT; MAMBA_CLIP_AMD_SIDE_TOWER=text/image overrides (A/B;
+        profiles/r04/stream_priority/)."""
+        env = os.environ.get("MAMBA_CLIP_AMD_SIDE_TOWER")
+        if env in ("text", "image"):
+            return env
+        return "text" if isinstance(self.text, BertTextEncoder) else "image"
+
+    def side_tower_module(self):
+        return self.visual if self.side_tower == "image" else self.text
 
     def side_stream_for(self, device):
         device = torch.device(device)
         if device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
-        key = (device, bool(self.side_high_priority))
+        key = (device, int(self.side_priority))
         if key not in ClipModel._side_streams:
-            ClipModel._side_streams[key] = torch.cuda.Stream(device=device, priority=-1 if key[1] else 0)
+            ClipModel._side_streams[key] = torch.cuda.Stream(device=device, priority=key[1])
         return ClipModel._side_streams[key]
 
     def _side_stream(self, image, text):
@@ -486,13 +500,21 @@ class ClipModel(nn.Module):
                 main = torch.cuda.current_stream()
                 self.last_main_stream = main                 # train._join_streams_allreduce joins it
                 side.wait_stream(main)                       # the one-launch weight casts, the inputs
-                text.record_stream(side)
                 casts.record_stream(side)
-                with torch.cuda.stream(side):
+                if self.side_tower == "image":
+                    image.record_stream(side)
+                    with torch.cuda.stream(side):
+                        image_features = self.encode_image(image, normalize=True)
                     text_features = self.encode_text(text, normalize=True)
-                image_features = self.encode_image(image, normalize=True)
-                main.wait_stream(side)
-                text_features.record_stream(main)
+                    main.wait_stream(side)
+                    image_features.record_stream(main)
+                else:
+                    text.record_stream(side)
+                    with torch.cuda.stream(side):
+                        text_features = self.encode_text(text, normalize=True)
+                    image_features = self.encode_image(image, normalize=True)
+                    main.wait_stream(side)
+                    text_features.record_stream(main)
             secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
         if self.output_dict:
             out = {"image_features": image_features, "text_features": text_features,

@@ -121,7 +121,7 @@ def wrap_ddp(model, args, device):
     if device.type == "cuda":
         kw["device_ids"] = [device]
     side = model.side_stream_for(device) if (device.type == "cuda" and hasattr(model, "side_stream_for")) else None
-    if side is not None and hasattr(model, "text"):
+    if side is not None and hasattr(model, "side_tower_module"):
         # DDP keeps every parameter's AccumulateGrad node alive from here on, and a node runs on the
         # stream current at its creation.  Created now on the main stream, each text-tower gradient
         # would make the main stream wait for the side stream's backward at that point (autograd's
@@ -129,7 +129,7 @@ def wrap_ddp(model, args, device):
         # text tower's gradients are accumulated (and DDP's bucket copies made) where they are produced.
         with torch.cuda.stream(side):
             model._side_grad_accumulators = [p.view_as(p).grad_fn.next_functions[0][0]
-                                             for p in model.text.parameters() if p.requires_grad]
+                                             for p in model.side_tower_module().parameters() if p.requires_grad]
     ddp = torch.nn.parallel.DistributedDataParallel(model, **kw)
     if side is not None:
         # ClipModel runs its text tower on a second stream; a bucket may then hold gradients written
