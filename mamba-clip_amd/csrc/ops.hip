@@ -1233,37 +1233,47 @@ template <typename TO>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const mc_cast_t_tile* __restrict__ tiles, TO* __restrict__ base) {
   __shared__ float tile[64][65];
   const mc_cast_t_tile t = tiles[blockIdx.x];
-  const int tid = threadIdx.x, r = tid >> 2, c0 = (tid & 3) * 16;
+  // loads: thread (r = tid >> 2, a = tid & 3) reads float4 a + 4k of source row r, so the four lanes of a
+  // row cover 64 contiguous bytes per instruction
+  const int tid = threadIdx.x, r = tid >> 2, a = tid & 3;
   const bool full = t.rows == 64 && t.cols == 64 && (t.src_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(t.src) & 15) == 0;
   if (full) {
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(t.src + (int64_t)r * t.src_ld + 4 * (a + 4 * k));
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float4 v = *reinterpret_cast<const float4*>(t.src + (int64_t)r * t.src_ld + c0 + 4 * k);
-      tile[r][c0 + 4 * k] = v.x; tile[r][c0 + 4 * k + 1] = v.y; tile[r][c0 + 4 * k + 2] = v.z; tile[r][c0 + 4 * k + 3] = v.w;
+      const int c = 4 * (a + 4 * k);
+      tile[r][c] = v[k].x; tile[r][c + 1] = v[k].y; tile[r][c + 2] = v[k].z; tile[r][c + 3] = v[k].w;
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      tile[r][c0 + k] = (r < t.rows && c0 + k < t.cols) ? t.src[(int64_t)r * t.src_ld + c0 + k] : 0.f;
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 4 * (a + 4 * k) + e;
+        tile[r][c] = (r < t.rows && c < t.cols) ? t.src[(int64_t)r * t.src_ld + c] : 0.f;
+      }
   }
   __syncthreads();
-  // output row j (= source column), 16 consecutive source rows
-  const int j = tid >> 2, i0 = (tid & 3) * 16;
-  TO* dst = base + t.dst_off + (int64_t)j * t.dst_ld + i0;
-  float v[16];
+  // stores: output row j (= source column), 8-element groups a and a + 4 (source rows 8 g .. 8 g + 7): the
+  // four lanes of a row write 64 contiguous bytes per instruction
+  const int j = tid >> 2;
+  TO* dst = base + t.dst_off + (int64_t)j * t.dst_ld;
+  const bool vec = full && (t.dst_ld & 7) == 0 && (reinterpret_cast<uintptr_t>(base + t.dst_off) & 15) == 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) v[k] = tile[i0 + k][j];
-  const bool vec = full && (t.dst_ld & 7) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
-  if (vec) {
-    float a[8], b[8];
+  for (int hlf = 0; hlf < 2; ++hlf) {
+    const int g = a + 4 * hlf;
+    float v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { a[k] = v[k]; b[k] = v[8 + k]; }
-    reinterpret_cast<uint4*>(dst)[0] = pack_f<TO>(a);
-    reinterpret_cast<uint4*>(dst)[1] = pack_f<TO>(b);
-  } else if (j < t.cols) {
+    for (int e = 0; e < 8; ++e) v[e] = tile[8 * g + e][j];
+    if (vec) {
+      *reinterpret_cast<uint4*>(dst + 8 * g) = pack_f<TO>(v);
+    } else if (j < t.cols) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (i0 + k < t.rows) dst[k] = from_f<TO>(v[k]);
+      for (int e = 0; e < 8; ++e)
+        if (8 * g + e < t.rows) dst[8 * g + e] = from_f<TO>(v[e]);
+    }
   }
 }
 }  // namespace
