@@ -68,23 +68,41 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
     const int v = lane + 64 * i;
     if (v < nvec) ld_f32v<V>(w + v * V, wr[i]);
   }
+  // the NEXT row's x / res_in in flight during this row's math (rows <= 1024 wide)
+  uint4 qx[NV];
+  float qr[NV][V];
+  auto load = [&](int row, uint4 (&a)[NV], float (&b)[NV][V]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = lane + 64 * i;
+      a[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int e = 0; e < V; ++e) b[i][e] = 0.f;
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        a[i] = ld16(x + off);
+        if (res_in) ld_f32v<V>(res_in + off, b[i]);
+      }
+    }
+  };
+  constexpr bool kPrefetch = NV <= 2;
+  if (kPrefetch && wave < rows) load(wave, qx, qr);
   for (int row = wave; row < rows; row += nwaves) {
+    uint4 nx[NV];
+    float nr[NV][V];
+    if constexpr (kPrefetch) {
+      if (row + nwaves < rows) load(row + nwaves, nx, nr);
+    } else {
+      load(row, qx, qr);
+    }
     float h[NV][V];
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int v = lane + 64 * i;
       if (v < nvec) {
-        const int64_t off = (int64_t)row * cols + v * V;
-        const uint4 q = ld16(x + off);
 #pragma unroll
-        for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(q, e);
-        if (res_in) {
-          float r[V];
-          ld_f32v<V>(res_in + off, r);
-#pragma unroll
-          for (int e = 0; e < V; ++e) h[i][e] += r[e];
-        }
+        for (int e = 0; e < V; ++e) h[i][e] = elem_f<T>(qx[i], e) + qr[i][e];
 #pragma unroll
         for (int e = 0; e < V; ++e) ss = fmaf(h[i][e], h[i][e], ss);
       }
@@ -102,6 +120,14 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
         for (int e = 0; e < V; ++e) o[e] = h[i][e] * rs * wr[i][e];
         st16(y + off, pack_f<T>(o));
         if (res_out) st_f32v<V>(res_out + off, h[i]);
+      }
+    }
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        qx[i] = nx[i];
+#pragma unroll
+        for (int e = 0; e < V; ++e) qr[i][e] = nr[i][e];
       }
     }
   }
@@ -249,7 +275,29 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
         for (int e = 0; e < V; ++e) br[i][e] = 0.f;
     }
   }
+  // the NEXT row's x / res in flight during this row's math (as the backward; rows <= 1024 wide)
+  uint4 qx[NV], qr[NV];
+  auto load = [&](int row, uint4 (&a)[NV], uint4 (&b)[NV]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = lane + 64 * i;
+      a[i] = b[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (v < nvec) {
+        const int64_t off = (int64_t)row * cols + v * V;
+        a[i] = ld16(x + off);
+        if (res) b[i] = ld16(res + off);
+      }
+    }
+  };
+  constexpr bool kPrefetch = NV <= 2;
+  if (kPrefetch && wave < rows) load(wave, qx, qr);
   for (int row = wave; row < rows; row += nwaves) {
+    uint4 nx[NV], nr[NV];
+    if constexpr (kPrefetch) {
+      if (row + nwaves < rows) load(row + nwaves, nx, nr);
+    } else {
+      load(row, qx, qr);
+    }
     float h[NV][V];
     float sum = 0.f;
 #pragma unroll
@@ -257,9 +305,9 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
       const int v = lane + 64 * i;
       if (v < nvec) {
         const int64_t off = (int64_t)row * cols + v * V;
-        const uint4 q = ld16(x + off);
+        const uint4 q = qx[i];
         if (res) {
-          const uint4 r = ld16(res + off);
+          const uint4 r = qr[i];
 #pragma unroll
           for (int e = 0; e < V; ++e) h[i][e] = to_f(from_f<T>(elem_f<T>(q, e) + elem_f<T>(r, e)));
           if (h_out) st16(h_out + off, pack_f<T>(h[i]));
@@ -293,6 +341,10 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
         for (int e = 0; e < V; ++e) o[e] = fmaf((h[i][e] - mu) * rs, wr[i][e], br[i][e]);
         st16(y + (int64_t)row * cols + v * V, pack_f<T>(o));
       }
+    }
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) { qx[i] = nx[i]; qr[i] = nr[i]; }
     }
   }
 }
