@@ -224,6 +224,17 @@ size_t mc_scan_fwd_workspace_bytes(int32_t batch, int32_t seqlen, int32_t dstate
 size_t mc_scan_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_t seqlen, int32_t dstate,
                                    int32_t n_groups);
 
+/* Which kernel family mc_scan_fwd / mc_scan_bwd run for these params (no launch; for tests and
+ * tooling): the lane-pair kernels (16-bit rows, dstate 16, seqlen % 8 == 0, 16-B aligned rows:
+ * scan_fwd_pair.hip / scan_bwd_pair.hip), the general chunked kernels, or the grouped-direction
+ * (SS2D) path.  NONE for an empty call. */
+#define MC_SCAN_KERNEL_NONE 0
+#define MC_SCAN_KERNEL_PAIR 1
+#define MC_SCAN_KERNEL_GENERIC 2
+#define MC_SCAN_KERNEL_DIRS 3
+int32_t mc_scan_fwd_kernel(const mc_scan_fwd_params* p);
+int32_t mc_scan_bwd_kernel(const mc_scan_bwd_params* p);
+
 int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream);
 int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream);
 

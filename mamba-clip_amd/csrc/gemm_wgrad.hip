@@ -1,0 +1,319 @@
+// gemm_wgrad.hip -- long-reduction weight-gradient GEMM of the towers' projections (bf16 / f16 in, fp32 out).
+//
+//   C[m][n] = sum_t A(t, m) B(t, n)      (M, N <= a few thousand; T = batch * tokens, tens of thousands)
+//
+// This is dW = G^T X of every Linear in the image / text towers' backward (reference: the towers behind
+// encode_image / encode_text, /root/reference/src/mamba_clip/model.py:1011-1017; built at model.py:1270):
+// G is the output gradient, X the saved input, T the token count (C2 ViT: 50,432).  The output is
+// small (<= 9 tiles of 256 x 256 for the 768-wide layers) and the reduction long, so the launch
+// splits T over S workgroups per output tile (S ~ 256 CUs / tiles), writes one fp32 partial tile per
+// split into a slab workspace and sums the S slabs in a fixed order (mc_sum_slabs): deterministic.
+//
+// Operand layouts (per operand, template flags):
+//  * token-major (TM): row t holds the features, A(t, m) = A[t * lda + m] -- a Linear's (tokens,
+//    features) activations / gradients.  The LDS tile is [64 t][256 features] (512-B rows, as the
+//    rows arrive from HBM) and MFMA fragments are read TRANSPOSED with ds_read_b64_tr_b16 (each lane
+//    gets 4 consecutive t of one feature; two reads make the 8 of a 16x16x32 operand);
+//  * feature-major (FM): row m holds the tokens, A(t, m) = A[m * lda + t] -- the Mamba mixer's
+//    channel-major activations.  The LDS tile is [256 features][64 t] (128-B rows) and fragments
+//    are plain ds_read_b128 row reads.
+// Both land in LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip); the image is
+// lane-linear, so the bank swizzle sits on the SOURCE address and the matching read:
+//  * TM: 16-B chunk c of row r lives at slot c ^ 2 s(r), s(r) = (r & 3) | ((r >> 3) & 1) << 2 --
+//    the 8 rows of a half-wave's transposed read (4 rows per 16-lane group, groups 8 rows apart)
+//    land on 8 distinct 32-B bank slots: conflict-free;
+//  * FM: chunk c of row r at slot c ^ ((r >> 1) & 7) (16 consecutive rows reading one chunk hit 16
+//    distinct 16-B bank slots; as sim_fp8_kernel).
+// Tile 256 x 256 x 64, 8 waves as 2 (m) x 4 (n), 128 x 64 per wave on v_mfma_f32_16x16x32_{bf16,f16}
+// (32 accumulators); two LDS stages of 64 KB, the next step's loads in flight across the step's
+// MFMAs (counted vmcnt, raw s_barrier), one workgroup per CU.
+#include <type_traits>
+
+#include "mc_common.h"
+#include "../../include/mc_gemm.h"
+
+extern "C" int mc_sum_slabs(int32_t s, int64_t n, const float* src, int64_t slab_stride, float* dst, void* stream);
+
+namespace mc {
+namespace wgrad {
+
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kThreads = 512;
+constexpr int kTileBytes = kBM * kBK * 2;       // one operand tile (32 KB)
+constexpr int kStage = 2 * kTileBytes;          // A + B (64 KB)
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+struct Args {
+  int M, N, T, splits, tiles_m, tiles_n, nk;
+  const char* A; const char* B;
+  int64_t lda, ldb;          // elements
+  float* C; int64_t ldc;     // output (splits == 1) or slab base (slab s at C + s * slab_stride)
+  int64_t slab_stride;
+};
+
+// One global_load_lds_dwordx4: 16 B per lane from gsrc to LDS byte address m0v + 16 * lane (m0v
+// wave-uniform).  asm, so hipcc's waitcnt pass does not drain it at the next LDS read; the loop
+// counts completion with its own vmcnt.  M0 is compiler-reserved: saved and restored here.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(m0v) : "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma(const s16x8& a, const s16x8& b, const f32x4& c) {
+  if constexpr (std::is_same<T, bf16_t>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ s16x8 cat8(s16x4 lo, s16x4 hi) {
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// swizzled 16-B slot of chunk c in row r
+__device__ __forceinline__ int tm_slot(int r, int c) { return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2))); }
+__device__ __forceinline__ int fm_slot(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// glds source pointers of one operand tile for this lane (kInstr = 4 per wave): TM rows of 512 B (two
+// rows per instruction), FM rows of 128 B (eight rows per instruction).  Features past `dim` are
+// clamped (their results are never stored); the token range is always in bounds (T % 64 == 0).
+template <bool kFM>
+__device__ __forceinline__ void tile_sources(const char* base, int64_t ld, int dim, int f0, int w, int lane,
+                                             const char* (&src)[4], int64_t& step_bytes) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pos = w * 4096 + j * 1024 + lane * 16;   // byte in the tile image
+    if constexpr (!kFM) {
+      const int r = pos >> 9, slot = (pos >> 4) & 31;   // row = token, 32 chunks of 8 features
+      const int c = tm_slot(r, slot);                   // involution: slot <-> chunk
+      const int f = min(f0 + 8 * c, dim - 8);
+      src[j] = base + ((int64_t)r * ld + f) * 2;
+    } else {
+      const int r = pos >> 7, slot = (pos >> 4) & 7;    // row = feature, 8 chunks of 8 tokens
+      const int c = fm_slot(r, slot);
+      const int f = min(f0 + r, dim - 1);
+      src[j] = base + ((int64_t)f * ld + 8 * c) * 2;
+    }
+  }
+  step_bytes = kFM ? (int64_t)kBK * 2 : (int64_t)kBK * ld * 2;
+}
+
+template <typename T, bool kAFM, bool kBFM>
+__global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const Args g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kStage];   // the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  // XCD-aware order: consecutive linear ids (same split, neighbouring tiles) share an XCD's L2
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int nwg = tiles * g.splits;
+  const int bid0 = blockIdx.x, xcd = bid0 & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid0 >> 3);
+  const int split = lin / tiles, tile = lin % tiles;
+  const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+  const int k_begin = (int)(((int64_t)split * g.nk) / g.splits), k_end = (int)(((int64_t)(split + 1) * g.nk) / g.splits);
+  const int nk = k_end - k_begin;
+
+  const char* srcA[4];
+  const char* srcB[4];
+  int64_t stepA, stepB;
+  tile_sources<kAFM>(g.A, g.lda, g.M, m0, w, lane, srcA, stepA);
+  tile_sources<kBFM>(g.B, g.ldb, g.N, n0, w, lane, srcB, stepB);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    srcA[j] += stepA * k_begin;
+    srcB[j] += stepB * k_begin;
+  }
+  const uint32_t lds_w = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)(lds) + 4096u * w);
+  auto issue = [&](int step) __attribute__((always_inline)) {   // K step `step` (local) into stage step & 1
+    const uint32_t la = lds_w + (uint32_t)(step & 1) * kStage, lb = la + kTileBytes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      glds16(srcA[j] + stepA * step, la + j * 1024);
+      glds16(srcB[j] + stepB * step, lb + j * 1024);
+    }
+  };
+
+  // ---- fragment read offsets (bytes within a stage's operand image)
+  // TM (transposed reads): lane l = 16 g + 4 q + p supplies row 8 g + 4 h + q (+ 32 kk), features
+  // [base + 4 p, +4): chunk base / 8 + (p >> 1), half 8 (p & 1).  s(r) = q | (g & 1) << 2 for every
+  // kk / h, so the slot XOR is a per-lane constant.
+  // FM (row reads): lane row (l & 15) of a 16-row tile, tokens [8 (l >> 4), +8) (+ 32 kk): chunk
+  // (l >> 4) + 4 kk.
+  const int fg = lane >> 4, fi = lane & 15, fq = fi >> 2, fp = fi & 3;
+  int offA[8], offB[4];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int base = wr * 128 + mi * 16;
+    if constexpr (!kAFM) {
+      const int r = 8 * fg + fq;
+      offA[mi] = r * 512 + (tm_slot(r, base / 8 + (fp >> 1)) << 4) + 8 * (fp & 1);
+    } else {
+      const int r = base + fi;
+      offA[mi] = r * 128;   // + slot (depends on kk) at the read
+    }
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int base = wc * 64 + ni * 16;
+    if constexpr (!kBFM) {
+      const int r = 8 * fg + fq;
+      offB[ni] = r * 512 + (tm_slot(r, base / 8 + (fp >> 1)) << 4) + 8 * (fp & 1);
+    } else {
+      const int r = base + fi;
+      offB[ni] = r * 128;
+    }
+  }
+  auto frag = [&](const char* img, int off, int row_for_fm, int kk, auto is_fm) __attribute__((always_inline)) -> s16x8 {
+    if constexpr (!decltype(is_fm)::value) {
+      const lds_char* p = (const lds_char*)(img) + off + kk * 32 * 512;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 512));
+      return cat8(lo, hi);
+    } else {
+      const int slot = fm_slot(row_for_fm, fg + 4 * kk);
+      return *reinterpret_cast<const s16x8*>(img + off + (slot << 4));
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  for (int s = 0; s < nk; ++s) {
+    // this wave's 8 loads of step s done (step s + 1's 8 may stay in flight), then everyone's
+    if (s + 1 < nk) __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8)
+    else __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    const char* la = lds + (s & 1) * kStage;
+    const char* lb = la + kTileBytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8 af[8], bfr[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        bfr[ni] = frag(lb, offB[ni], wc * 64 + ni * 16 + fi, kk, std::integral_constant<bool, kBFM>());
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+        af[mi] = frag(la, offA[mi], wr * 128 + mi * 16 + fi, kk, std::integral_constant<bool, kAFM>());
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma<T>(af[mi], bfr[ni], acc[mi][ni]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();         // ... and everyone's: the stage can be refilled
+    if (s + 2 < nk) issue(s + 2);
+  }
+
+  // ---- epilogue: fp32 tile (or this split's partial tile) -> C / slab.  acc[mi][ni] lane l holds
+  // rows 4 (l >> 4) + [0, 4) and column l & 15 of its 16 x 16 block.
+  float* C = g.C + (int64_t)split * g.slab_stride;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wc * 64 + ni * 16 + fi;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 128 + mi * 16 + 4 * fg + r;
+        if (row < g.M && col < g.N) C[(int64_t)row * g.ldc + col] = acc[mi][ni][r];
+      }
+    }
+}
+
+template <typename T>
+static void launch_t(const Args& a, bool afm, bool bfm, hipStream_t s) {
+  const dim3 grid(a.tiles_m * a.tiles_n * a.splits), block(kThreads);
+  if (!afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, false>), grid, block, 0, s, a);
+  else if (!afm && bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, true>), grid, block, 0, s, a);
+  else if (afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, true, false>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<T, true, true>), grid, block, 0, s, a);
+}
+
+static int auto_splits(int tiles, int nk) {
+  // about one workgroup per CU (256), at least 4 K steps per split
+  int s = (256 + tiles / 2) / tiles;
+  s = std::max(1, std::min(s, nk / 4));
+  return s;
+}
+
+}  // namespace wgrad
+}  // namespace mc
+
+using namespace mc;
+using namespace mc::wgrad;
+
+static int resolve(const mc_wgrad_params* p, int& splits, int& tiles_m, int& tiles_n, int& nk) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_gemm_wgrad: null params");
+  MC_CHECK(p->M > 0 && p->N > 0 && p->T >= 0, MC_ERR_SHAPE, "mc_gemm_wgrad: bad shape M %d N %d T %d", p->M, p->N, p->T);
+  MC_CHECK(p->dtype == MC_DTYPE_BF16 || p->dtype == MC_DTYPE_F16, MC_ERR_DTYPE, "mc_gemm_wgrad: operands must be bf16 or f16");
+  MC_CHECK(p->T % kBK == 0, MC_ERR_SHAPE, "mc_gemm_wgrad: T %d must be a multiple of %d", p->T, kBK);
+  MC_CHECK(p->a_layout == MC_WGRAD_TOKEN_MAJOR || p->a_layout == MC_WGRAD_FEATURE_MAJOR, MC_ERR_INVALID,
+           "mc_gemm_wgrad: bad a_layout %d", p->a_layout);
+  MC_CHECK(p->b_layout == MC_WGRAD_TOKEN_MAJOR || p->b_layout == MC_WGRAD_FEATURE_MAJOR, MC_ERR_INVALID,
+           "mc_gemm_wgrad: bad b_layout %d", p->b_layout);
+  auto ok = [&](const void* t, int64_t ld, int dim, int layout) {
+    const int64_t rows = layout == MC_WGRAD_TOKEN_MAJOR ? p->T : dim;
+    const int64_t cols = layout == MC_WGRAD_TOKEN_MAJOR ? dim : p->T;
+    return t && aligned16(t) && ld % 8 == 0 && ld >= cols && (layout != MC_WGRAD_TOKEN_MAJOR || dim % 8 == 0) &&
+           rows * ld < ((int64_t)1 << 40);
+  };
+  MC_CHECK(ok(p->A, p->lda, p->M, p->a_layout) && ok(p->B, p->ldb, p->N, p->b_layout), MC_ERR_SHAPE,
+           "mc_gemm_wgrad: operands need 16-B aligned bases, leading dims %% 8 == 0 and >= the row length, and "
+           "token-major feature counts %% 8 == 0 (M %d lda %lld, N %d ldb %lld)", p->M, (long long)p->lda, p->N,
+           (long long)p->ldb);
+  MC_CHECK(p->C && p->ldc == p->N, MC_ERR_SHAPE, "mc_gemm_wgrad: C must be a contiguous M x N fp32 matrix");
+  tiles_m = (p->M + kBM - 1) / kBM;
+  tiles_n = (p->N + kBN - 1) / kBN;
+  nk = p->T / kBK;
+  splits = p->splits > 0 ? std::min(p->splits, std::max(nk, 1)) : auto_splits(tiles_m * tiles_n, nk);
+  return MC_OK;
+}
+
+extern "C" size_t mc_gemm_wgrad_workspace_bytes(const mc_wgrad_params* p) {
+  int splits, tm, tn, nk;
+  if (resolve(p, splits, tm, tn, nk) != MC_OK) return 0;
+  return splits > 1 ? (size_t)splits * p->M * p->N * 4 : 0;
+}
+
+extern "C" int mc_gemm_wgrad(const mc_wgrad_params* p, void* stream) {
+  int splits, tiles_m, tiles_n, nk;
+  int rc = resolve(p, splits, tiles_m, tiles_n, nk);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (nk == 0) {
+    (void)hipMemsetAsync(p->C, 0, (size_t)p->M * p->N * 4, s);
+    return MC_OK;
+  }
+  const size_t ws_need = splits > 1 ? (size_t)splits * p->M * p->N * 4 : 0;
+  MC_CHECK(ws_need == 0 || (p->workspace && p->workspace_bytes >= ws_need && aligned16(p->workspace)), MC_ERR_WORKSPACE,
+           "mc_gemm_wgrad: workspace must be >= %zu bytes, 16-B aligned (got %zu)", ws_need, p->workspace_bytes);
+  Args a;
+  a.M = p->M; a.N = p->N; a.T = p->T; a.splits = splits; a.tiles_m = tiles_m; a.tiles_n = tiles_n; a.nk = nk;
+  a.A = reinterpret_cast<const char*>(p->A); a.B = reinterpret_cast<const char*>(p->B);
+  a.lda = p->lda; a.ldb = p->ldb;
+  a.C = splits > 1 ? reinterpret_cast<float*>(p->workspace) : p->C;
+  a.ldc = p->N;
+  a.slab_stride = (int64_t)p->M * p->N;
+  const bool afm = p->a_layout == MC_WGRAD_FEATURE_MAJOR, bfm = p->b_layout == MC_WGRAD_FEATURE_MAJOR;
+  if (p->dtype == MC_DTYPE_BF16) launch_t<bf16_t>(a, afm, bfm, s);
+  else launch_t<f16_t>(a, afm, bfm, s);
+  hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_wgrad: launch failed: %s", hipGetErrorString(e));
+  if (splits > 1) return mc_sum_slabs(splits, (int64_t)p->M * p->N, a.C, a.slab_stride, p->C, stream);
+  return MC_OK;
+}

@@ -849,6 +849,12 @@ extern "C" size_t mc_scan_bwd_workspace_bytes(int32_t batch, int32_t dim, int32_
   return bwd_ws_layout(batch, dim, seqlen, dstate, n_groups).total;
 }
 
+extern "C" int32_t mc_scan_bwd_kernel(const mc_scan_bwd_params* p) {
+  if (!p || p->batch == 0 || p->seqlen == 0) return MC_SCAN_KERNEL_NONE;
+  if (p->reverse_groups != 0 || p->u_groups != 0) return MC_SCAN_KERNEL_DIRS;
+  return bwd_pair_ok(p) ? MC_SCAN_KERNEL_PAIR : MC_SCAN_KERNEL_GENERIC;
+}
+
 extern "C" int mc_scan_bwd(const mc_scan_bwd_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_scan_bwd: null params");
   int rc = validate_common(p->batch, p->dim, p->seqlen, p->dstate, p->n_groups, p->itype, p->wtype, "mc_scan_bwd");

@@ -820,6 +820,14 @@ extern "C" int mc_scan_fwd(const mc_scan_fwd_params* p, void* stream) {
   return launch_fwd_t<f16_t>(a, aligned, s);
 }
 
+extern "C" int32_t mc_scan_fwd_kernel(const mc_scan_fwd_params* p) {
+  if (!p || p->batch == 0 || p->seqlen == 0) return MC_SCAN_KERNEL_NONE;
+  if (p->reverse_groups != 0 || p->u_groups != 0) return MC_SCAN_KERNEL_DIRS;
+  FwdArgs a;
+  bool aligned = false;
+  return fill_fwd_args(p, a, aligned) ? MC_SCAN_KERNEL_PAIR : MC_SCAN_KERNEL_GENERIC;
+}
+
 extern "C" int32_t mc_scan_fwd_state_interval(const mc_scan_fwd_params* p) {
   if (!p || p->state_interval != kFineS) return kS;
   FwdArgs a;

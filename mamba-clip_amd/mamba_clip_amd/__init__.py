@@ -14,8 +14,10 @@ __version__ = "0.1.0"
 # several workgroups, the first of which waits for the others' partial sums -- so every workgroup of
 # the launch must be co-resident.  Two such launches on two streams can each hold part of the CUs and
 # wait forever (the round-3 C3 hang).  TENSILE_STREAMK_DATA_PARALLEL=1 makes hipBLASLt launch one
-# workgroup per tile (tools/sk_probe.sh: 0 of the 440 C2 / 299 C3 step GEMMs split a tile, against
-# 253 / 121 by default, GEMM time unchanged), and then no GEMM workgroup waits on another.
+# workgroup per tile (tools/sk_probe.sh, profiles/r04/sk_probe/: with it 0 of the 440 C2 / 299 C3
+# step GEMM dispatches split a tile's K range, against 36 / 13 by default -- the sweeps' larger
+# 253 / 121 counts also include stream-K launches that run whole tiles -- GEMM time unchanged), and
+# then no GEMM workgroup waits on another.
 # hipBLASLt reads the variable once, on its first GEMM, so it is set here, before this process can
 # have run one -- unless CUDA was already live at import, in which case it may be too late.
 _SK_ENV = "TENSILE_STREAMK_DATA_PARALLEL"

@@ -15,6 +15,7 @@ MC_DTYPE_F32, MC_DTYPE_BF16, MC_DTYPE_F16, MC_DTYPE_FP8_E4M3, MC_DTYPE_U8 = 0, 1
 MC_LAYOUT_NCHW, MC_LAYOUT_NHWC = 0, 1
 MC_SCAN_CHUNK = 32
 MC_SCAN_STATE_INTERVAL_FINE = 8
+MC_SCAN_KERNEL_NONE, MC_SCAN_KERNEL_PAIR, MC_SCAN_KERNEL_GENERIC, MC_SCAN_KERNEL_DIRS = 0, 1, 2, 3
 MC_SCAN_MAX_DSTATE = 32
 MC_CAST_CHUNK = 16384
 
@@ -200,6 +201,18 @@ class SS2DMergeBwdParams(ctypes.Structure):
     ]
 
 
+MC_WGRAD_TOKEN_MAJOR, MC_WGRAD_FEATURE_MAJOR = 0, 1
+
+
+class WgradParams(ctypes.Structure):
+    """Mirror of ``mc_wgrad_params`` (include/mc_gemm.h)."""
+    _fields_ = [
+        ("M", c_i32), ("N", c_i32), ("T", c_i32), ("dtype", c_i32), ("a_layout", c_i32), ("b_layout", c_i32),
+        ("A", c_vp), ("lda", c_i64), ("B", c_vp), ("ldb", c_i64), ("C", c_vp), ("ldc", c_i64),
+        ("splits", c_i32), ("reserved", c_i32), ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 class PatchInputParams(ctypes.Structure):
     """Mirror of ``mc_patch_input_params`` (include/mc_ops.h)."""
     _fields_ = [
@@ -216,6 +229,10 @@ SYMBOLS = {
     "mc_scan_n_chunks": (c_i32, [c_i32]),
     "mc_scan_n_states": (c_i32, [c_i32, c_i32]),
     "mc_scan_fwd_state_interval": (c_i32, [ctypes.POINTER(ScanFwdParams)]),
+    "mc_scan_fwd_kernel": (c_i32, [ctypes.POINTER(ScanFwdParams)]),
+    "mc_gemm_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradParams)]),
+    "mc_gemm_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradParams), c_vp]),
+    "mc_scan_bwd_kernel": (c_i32, [ctypes.POINTER(ScanBwdParams)]),
     "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),

@@ -669,10 +669,57 @@ def _split_factor(M, N, K):
     return s
 
 
+def _wgrad_layout(t, rows_are_tokens):
+    """(layout, leading dim) of a 2-D operand for mc_gemm_wgrad, or None when neither dim is unit-stride.
+    rows_are_tokens: t is (T, features) (X); else (features, T) (G)."""
+    st_tok, st_feat = (t.stride(0), t.stride(1)) if rows_are_tokens else (t.stride(1), t.stride(0))
+    if st_feat == 1 and t.shape[1 if rows_are_tokens else 0] > 0:
+        return _lib.MC_WGRAD_TOKEN_MAJOR, st_tok
+    if st_tok == 1:
+        return _lib.MC_WGRAD_FEATURE_MAJOR, st_feat
+    return None
+
+
+def wgrad_hip(G, X, splits=0):
+    """G @ X in fp32 on the hand-written long-reduction GEMM (csrc/gemm_wgrad.hip, mc_gemm_wgrad):
+    G (N, T) and X (T, K), 16-bit, each with one unit-stride dim; returns None when the shape or
+    layout is outside the kernel's (T % 64, 16-B aligned rows), so the caller takes the library path."""
+    if not (G.is_cuda and G.dtype == X.dtype and G.dtype in (torch.bfloat16, torch.float16)):
+        return None
+    N, T = G.shape
+    K = X.shape[1]
+    la, lb = _wgrad_layout(G, False), _wgrad_layout(X, True)
+    if la is None or lb is None or T % 64 or T == 0 or G.data_ptr() % 16 or X.data_ptr() % 16:
+        return None
+    if la[1] % 8 or lb[1] % 8 or (la[0] == _lib.MC_WGRAD_TOKEN_MAJOR and N % 8) or \
+            (lb[0] == _lib.MC_WGRAD_TOKEN_MAJOR and K % 8):
+        return None
+    out = torch.empty(N, K, device=G.device, dtype=torch.float32)
+    p = _lib.WgradParams()
+    p.M, p.N, p.T, p.dtype = N, K, T, _lib.dtype_code(G.dtype)
+    p.a_layout, p.lda, p.b_layout, p.ldb = la[0], la[1], lb[0], lb[1]
+    p.A, p.B, p.C, p.ldc, p.splits = G.data_ptr(), X.data_ptr(), out.data_ptr(), K, int(splits)
+    lib = _lib.load()
+    ws_b = lib.mc_gemm_wgrad_workspace_bytes(ctypes.byref(p))
+    ws = _ws(ws_b, G.device) if ws_b else None
+    if ws is not None:
+        p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+    _lib.check(lib.mc_gemm_wgrad(ctypes.byref(p), _lib.stream_handle(G.device)), "mc_gemm_wgrad")
+    return out
+
+
+# A/B toggle: the towers' weight gradients on mc_gemm_wgrad (1) or the library's split-K slabs (0)
+WGRAD_HIP = os.environ.get("MAMBA_CLIP_AMD_WGRAD_HIP", "0") != "0"
+
+
 def wgrad(G, X):
     """G @ X in fp32 for G (N, M), X (M, K), any strides, M the long reduction dim."""
     N, M = G.shape
     K = X.shape[1]
+    if WGRAD_HIP and G.is_cuda and M >= 8192:
+        out = wgrad_hip(G, X)
+        if out is not None:
+            return out
     s = _split_factor(M, N, K) if (G.is_cuda and M >= 8192) else 1
     if s == 1:
         return torch.mm(G, X).float()

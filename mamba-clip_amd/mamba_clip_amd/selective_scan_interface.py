@@ -12,6 +12,7 @@ fp32 chunk states (one per MC_SCAN_CHUNK positions); the backward runs
 synchronise.  There is no CPU / eager fallback.
 """
 import os
+import weakref
 
 import torch
 
@@ -59,10 +60,25 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
 
 
 def fine_states_max_bytes():
-    """Largest saved-state buffer (bytes, one scan call) kept at the fine interval: 4x the default
-    interval's memory buys the backward's recompute pass (C2 layer: 252 MB; a C4 layer at L 4096 would
-    be 6.4 GB and keeps the default).  MAMBA_CLIP_AMD_FINE_STATES_MB overrides (0 = never)."""
-    return int(float(os.environ.get("MAMBA_CLIP_AMD_FINE_STATES_MB", "1024")) * (1 << 20))
+    """Budget (bytes) for the fine saved states alive at once, over every scan call of the process (a
+    whole training step's layers, not one call).  The fine interval costs 4x the default interval's
+    memory and buys the backward's recompute pass: a C2 layer holds 252 MB of fine states instead of
+    63 MB, 6.0 GB instead of 1.5 GB for the 24 layers; a C4 layer (L 4096) would need 6.4 GB.  Calls
+    that would take the live total past the budget save the default interval instead (later layers of
+    a larger batch degrade gracefully rather than run out of memory).  MAMBA_CLIP_AMD_FINE_STATES_MB
+    sets it (default 8192 MB = C2 at batch 256 plus margin; 0 = never)."""
+    return int(float(os.environ.get("MAMBA_CLIP_AMD_FINE_STATES_MB", "8192")) * (1 << 20))
+
+
+_FINE_LIVE = [0]   # bytes of fine saved states currently alive (released when the tensor is freed)
+
+
+def _fine_release(nbytes):
+    _FINE_LIVE[0] -= nbytes
+
+
+def fine_states_live_bytes():
+    return _FINE_LIVE[0]
 
 
 def states_interval(L, dim, states):
@@ -137,13 +153,19 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
         # the fine saved-state interval where the pair kernel runs and the states fit the budget:
         # the backward then reads each sub-tile's entry state instead of recomputing it
         fine = _lib.MC_SCAN_STATE_INTERVAL_FINE
-        if batch * dim * lib.mc_scan_n_states(L, fine) * dstate * 4 <= fine_states_max_bytes():
+        fine_bytes = batch * dim * lib.mc_scan_n_states(L, fine) * dstate * 4
+        if _FINE_LIVE[0] + fine_bytes <= fine_states_max_bytes():
             p.state_interval = fine
             p.state_interval = lib.mc_scan_fwd_state_interval(p)
         nch = lib.mc_scan_n_states(L, p.state_interval)
         shape = (batch, nch, dim, dstate) if p.state_interval == fine else (batch, dim, nch, dstate)
         states = torch.empty(shape, device=u.device, dtype=torch.float32)
+        if p.state_interval == fine:
+            _FINE_LIVE[0] += fine_bytes
+            weakref.finalize(states, _fine_release, fine_bytes)
         p.chunk_states = states.data_ptr()
+    if RECORD_DISPATCH:
+        DISPATCH.append(("fwd", int(lib.mc_scan_fwd_kernel(p))))
     _lib.check(lib.mc_scan_fwd(p, _lib.stream_handle(u.device)), "mc_scan_fwd")
     if want_last and states is not None:
         if nch == 0:
@@ -153,6 +175,12 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
     if want_y:
         return out, states, last, out_y
     return out, states, last
+
+
+# Tests set RECORD_DISPATCH to see which kernel family (_lib.MC_SCAN_KERNEL_*) each call ran:
+# DISPATCH collects ("fwd" | "bwd", code) per launch (mc_scan_fwd_kernel / mc_scan_bwd_kernel).
+RECORD_DISPATCH = False
+DISPATCH = []
 
 
 def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, dirs=None, dz_out=None, proj=None,
@@ -215,6 +243,8 @@ def scan_bwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, states, 
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws_bytes
     if dirs is not None:
         p.reverse_groups, p.u_groups = int(dirs[0]), int(dirs[1])
+    if RECORD_DISPATCH:
+        DISPATCH.append(("bwd", int(lib.mc_scan_bwd_kernel(p))))
     _lib.check(lib.mc_scan_bwd(p, _lib.stream_handle(u.device)), "mc_scan_bwd")
     return du, ddelta, dA, dB, dC, dD, dz, dbias
 

@@ -108,6 +108,13 @@ SCAN_CASES = {
     "f16_z_g2": (2, 64, 64, 16, 2, torch.float16, torch.float32, True, True, True, True, True, True),
     "len1_f32": (3, 64, 1, 4, 1, torch.float32, torch.float32, True, True, True, True, True, True),
     "ragged_ch_f32": (2, 96, 45, 16, 3, torch.float32, torch.bfloat16, True, True, True, True, True, True),
+    # the shipped lane-pair kernels' shapes (scan_fwd_pair.hip / scan_bwd_pair.hip: 16-bit rows and
+    # B / C, N = 16, L % 8 == 0, G = 1): C2's text tower (77 tokens padded to 80, 3 chunks, the last
+    # half masked), a 256-position and a 1024-position sequence (the C4 regime at a small width)
+    "pair_c2_l80_bf16": (2, 64, 80, 16, 1, torch.bfloat16, torch.bfloat16, True, True, True, True, True, False),
+    "pair_l256_bf16": (2, 64, 256, 16, 1, torch.bfloat16, torch.bfloat16, True, True, True, True, True, True),
+    "pair_l1024_bf16": (1, 32, 1024, 16, 1, torch.bfloat16, torch.bfloat16, True, True, True, True, True, True),
+    "pair_l128_f16_3d": (2, 64, 128, 16, 1, torch.float16, torch.float16, True, True, True, True, False, False),
 }
 
 
@@ -124,6 +131,10 @@ def gen_scan(ref_scan):
         args = {k: leaves.get(k) for k in x}
         gout = ref_scan(**args, delta_softplus=sp)
         dout = torch.randn(gout.shape, generator=gen)
+        if name.startswith("pair_"):
+            # the pair-kernel cases are compared with these gradients directly: dout as the 16-bit
+            # output gradient autograd hands the kernel (exactly representable in itype)
+            dout = dout.to(itype).float()
         gout.backward(dout)
         tensors = {f"in.{k}": v.contiguous() for k, v in x.items() if v is not None}
         tensors["out"] = out.contiguous()

@@ -65,6 +65,33 @@ def test_validation_errors_without_launch():
         _lib.check(lib.mc_scan_fwd(ctypes.byref(p), None), "mc_scan_fwd")
 
 
+def test_wgrad_validation_without_launch():
+    """mc_gemm_wgrad rejects bad shapes / layouts on the host; workspace sizing is host-only."""
+    from mamba_clip_amd import _lib
+    lib = _lib.load()
+    p = _lib.WgradParams()
+    p.M, p.N, p.T, p.dtype = 768, 768, 100, _lib.MC_DTYPE_BF16        # T % 64 != 0
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -3 and b"multiple of 64" in lib.mc_last_error()
+    p.T, p.dtype = 50432, _lib.MC_DTYPE_F32
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -2
+    p.dtype, p.a_layout = _lib.MC_DTYPE_BF16, 7
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -1
+    p.a_layout = _lib.MC_WGRAD_TOKEN_MAJOR
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -3             # null operands
+    p.A = p.B = p.C = 4096
+    p.lda = p.ldb = 768
+    p.ldc = 769
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -3 and b"contiguous" in lib.mc_last_error()
+    p.ldc = 768
+    # 9 output tiles of 256 x 256 -> about one workgroup per CU: 28 splits of fp32 slabs
+    assert lib.mc_gemm_wgrad_workspace_bytes(ctypes.byref(p)) == 28 * 768 * 768 * 4
+    p.splits = 1
+    assert lib.mc_gemm_wgrad_workspace_bytes(ctypes.byref(p)) == 0
+    p.splits = 0
+    p.workspace, p.workspace_bytes = 4096, 16
+    assert lib.mc_gemm_wgrad(ctypes.byref(p), None) == -5             # workspace too small
+
+
 def test_fused_ce_validation_without_launch():
     """mc_ce_fused_fwd / _grad reject bad arguments on the host."""
     from mamba_clip_amd import _lib
@@ -122,13 +149,14 @@ def test_attention_validation_without_launch():
                                           ("mc_ss2d_merge_bwd_params", "SS2DMergeBwdParams"),
                                           ("mc_patch_input_params", "PatchInputParams"),
                                           ("mc_mixer_proj_params", "MixerProjParams"),
-                                          ("mc_mixer_proj_bwd_params", "MixerProjBwdParams")])
+                                          ("mc_mixer_proj_bwd_params", "MixerProjBwdParams"),
+                                          ("mc_wgrad_params", "WgradParams")])
 def test_struct_layout_matches_header(cname, pyname):
     from mamba_clip_amd import _lib
     cls = getattr(_lib, pyname)
     fields = [f for f, _ in cls._fields_]
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mc_scan.h"', '#include "mc_contrastive.h"',
-           '#include "mc_ops.h"', '#include "mc_attn.h"', '#include "mc_ss2d.h"',
+           '#include "mc_ops.h"', '#include "mc_attn.h"', '#include "mc_ss2d.h"', '#include "mc_gemm.h"',
            "int main(void){",
            f'printf("size %zu\\n", sizeof({cname}));']
     src += [f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields]

@@ -93,3 +93,67 @@ def test_hip_adamw_skips_params_without_grad_and_rejects_fp16():
     h.grad = torch.ones_like(h)
     with pytest.raises(RuntimeError, match="fp32"):
         o2.step()
+
+
+def test_hip_adamw_per_parameter_steps_match_torch():
+    """step counts are per parameter.  A parameter that skips a step keeps its count and
+    bias corrections, one whose first gradient comes late starts at 1, and a torch state dict whose
+    parameters of one group have different counts loads and resumes (torch AdamW, single-tensor path,
+    as the oracle)."""
+    from mamba_clip_amd.optim import HipAdamW
+    a, b = _params(3), _params(3)
+    oa = HipAdamW(_groups(a), lr=1e-3, betas=(0.9, 0.98), eps=1e-6)
+    ob = torch.optim.AdamW(_groups(b), lr=1e-3, betas=(0.9, 0.98), eps=1e-6, foreach=False)
+    # step k: which parameters get a gradient (param 1 skips step 1, param 4 starts at step 2, ...)
+    plan = [{0, 1, 3, 5}, {0, 3, 5, 6}, {0, 1, 3, 4, 5, 6}, {1, 2, 4}, set(range(7))]
+    for k, have in enumerate(plan):
+        for ps in (a, b):
+            grads = _grads(ps, 300 + k)
+            for i, p in enumerate(ps):
+                p.grad = grads[i] if i in have else None
+        oa.step()
+        ob.step()
+    for i, (pa, pb) in enumerate(zip(a, b)):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=f"param {i}")
+        assert float(oa.state[pa]["step"]) == float(ob.state[pb]["step"]), i
+    # torch's state (different step counts inside each group) -> a fresh HipAdamW, two more steps
+    c = _params(3)
+    with torch.no_grad():
+        for pc, pb in zip(c, b):
+            pc.copy_(pb)
+    oc = HipAdamW(_groups(c), lr=1e-3, betas=(0.9, 0.98), eps=1e-6)
+    oc.load_state_dict(copy.deepcopy(ob.state_dict()))
+    for k in range(2):
+        for ps in (b, c):
+            for p, gr in zip(ps, _grads(ps, 400 + k)):
+                p.grad = gr
+        ob.step()
+        oc.step()
+    for i, (pc, pb) in enumerate(zip(c, b)):
+        torch.testing.assert_close(pc, pb, rtol=1e-5, atol=1e-6, msg=f"param {i}")
+        assert float(oc.state[pc]["step"]) == float(ob.state[pb]["step"]), i
+    # the saved form is torch's: one step tensor per parameter
+    sd = oc.state_dict()
+    steps = [v["step"] for v in sd["state"].values()]
+    assert len({id(t) for t in steps}) == len(steps)
+
+
+def test_hip_adamw_many_buckets_split_launches():
+    """More (group, step) buckets than MC_ADAMW_MAX_GROUPS: several launches, same result as torch."""
+    from mamba_clip_amd import _lib
+    from mamba_clip_amd.optim import HipAdamW
+    n = _lib.MC_ADAMW_MAX_GROUPS + 3
+    g = torch.Generator(device=DEV).manual_seed(9)
+    a = [torch.randn(1000 + 7 * i, device=DEV, generator=g).requires_grad_(True) for i in range(n)]
+    b = [p.detach().clone().requires_grad_(True) for p in a]
+    oa = HipAdamW([{"params": [p]} for p in a], lr=1e-3)
+    ob = torch.optim.AdamW([{"params": [p]} for p in b], lr=1e-3, foreach=False)
+    for k in range(n):            # parameter i starts at step i: n distinct step counts at the end
+        for ps in (a, b):
+            grads = _grads(ps, 500 + k)
+            for i, p in enumerate(ps):
+                p.grad = grads[i] if i <= k else None
+        oa.step()
+        ob.step()
+    for pa, pb in zip(a, b):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)

@@ -450,3 +450,40 @@ def test_scan_bwd_generic_kernel_reads_fine_states():
     got = dict(u=du, delta=ddelta, A=dA, B=dB, C=dC, D=dD, z=dz, delta_bias=dbias)
     for k, g in ref.items():
         assert_grad_close(got[k], g, torch.bfloat16 if k in ("u", "delta", "z", "B", "C") else torch.float32, k)
+
+
+# ----------------------------------------------------------------- the shipped pair kernels vs the reference text
+PAIR_FILES = [f for f in SCAN_FILES if f.startswith("scan_pair_")]
+
+
+@pytest.mark.parametrize("fine_mb", ["1024", "0"], ids=["fine_states", "chunk_states"])
+@pytest.mark.parametrize("fname", PAIR_FILES)
+def test_pair_kernels_match_reference_text_golden(fname, fine_mb, monkeypatch):
+    """golden vectors executed from the reference's own text (model.py:83-169)
+    at the lane-pair kernels' shapes (16-bit rows, N = 16, L % 8 == 0, incl. C2's padded L = 80).
+    Asserts that the pair kernels are the ones dispatched (mc_scan_fwd_kernel / mc_scan_bwd_kernel),
+    at both saved-state intervals, and compares output, last state and every gradient directly with
+    the reference text's fp32 values (16-bit outputs within one ulp of their dtype + 2e-4 of max)."""
+    from mamba_clip_amd import _lib
+    from mamba_clip_amd import selective_scan_interface as ssi
+    monkeypatch.setenv("MAMBA_CLIP_AMD_FINE_STATES_MB", fine_mb)
+    monkeypatch.setattr(ssi, "RECORD_DISPATCH", True)
+    monkeypatch.setattr(ssi, "DISPATCH", [])
+    g = load_golden(fname)
+    meta = golden_meta(fname)
+    sp, last = meta["softplus"] == "1", meta["last"] == "1"
+    leaves = {k[3:]: v.to(DEV).requires_grad_(True) for k, v in g.items() if k.startswith("in.")}
+    res = ssi.selective_scan_fn(**leaves, delta_softplus=sp, return_last_state=last)
+    out, ls = res if last else (res, None)
+    assert_scan_close(out, g["out_f32"], out.dtype)
+    if last:
+        assert_scan_close(ls, g["last_state"], torch.float32, "last_state")
+    out.backward(g["dout"].to(DEV).to(out.dtype))
+    assert ssi.DISPATCH == [("fwd", _lib.MC_SCAN_KERNEL_PAIR), ("bwd", _lib.MC_SCAN_KERNEL_PAIR)], ssi.DISPATCH
+    for k, v in leaves.items():
+        ref = g[f"grad.{k}"]
+        dt = v.grad.dtype
+        assert v.grad.shape == ref.shape, k
+        # the reference's gradient used dout in fp32, ours the 16-bit-rounded dout: that rounding
+        # is inside the dtype's ulp term
+        assert_grad_close(v.grad, ref, dt, "reference-text " + k)

@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Run-to-run determinism of the training step, variant by variant.
+
+One process builds the C2 model once, then for each variant and repeat restores the initial
+parameters, builds a fresh optimizer and runs --steps optimizer steps on the same resident batch.
+Repeat 0 of the first variant is the reference; every later run reports, bitwise:
+  - step-1 image / text features and loss,
+  - step-1 gradients (first differing parameter names per tower),
+  - final parameters.
+Variants (comma list, --variants):
+  conc      towers on two streams (the default path)
+  seq       one stream
+  conc_sync two streams, device synchronize after forward and after backward
+  conc_torchadam  two streams, torch's fused AdamW instead of HipAdamW
+  conc_text two streams, text tower on the side stream
+  conc_nowt two streams, no transposed weight copies (ops.WCAST_T off)
+Run once as is and once with PYTORCH_NO_CUDA_MEMORY_CACHING=1 to separate allocator-reuse hazards
+(a missing record_stream) from ordering hazards (a missing wait)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="vit_b16-mamba130m")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--variants", default="conc,seq,conc_sync,conc_torchadam,conc_text,conc_nowt")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--compare", choices=["first", "prev"], default="first",
+                    help="compare each run with the first run overall, or with the previous run of its variant")
+    ap.add_argument("--fill-nan", action="store_true",
+                    help="torch.use_deterministic_algorithms(warn_only) + fill_uninitialized_memory: every torch.empty "
+                         "is NaN-filled, so a kernel reading memory it never wrote shows up")
+    args = ap.parse_args()
+    if args.fill_nan:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.utils.deterministic.fill_uninitialized_memory = True
+
+    from types import SimpleNamespace
+    from mamba_clip_amd import ops, train
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import ClipModel, build_clip
+    from mamba_clip_amd.tuning import load_gemm_tuning
+    from mamba_clip_amd.utils.amp_utils import get_autocast
+
+    dev = torch.device("cuda", 0)
+    load_gemm_tuning(model=args.model)
+    targs = SimpleNamespace(precision="amp_bf16", lr=5e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
+                            grad_clip_norm=None, accum_freq=1)
+    torch.manual_seed(0)
+    model = build_clip(args.model).to(dev)
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    images, texts, targets = synthetic_batch(args.batch, 224, model.text.context_length, model.text.vocab_size,
+                                             device=dev, seed=1000)
+    loss_fn = ClipLoss()
+    autocast = get_autocast(targs.precision)
+    names = [n for n, _ in model.named_parameters()]
+    img_names = {n for n in names if n.startswith("visual.")}
+
+    def run(variant):
+        model.load_state_dict(init)
+        model.zero_grad(set_to_none=True)
+        model.concurrent_towers = not variant.startswith("seq")
+        os.environ.pop("MAMBA_CLIP_AMD_SIDE_TOWER", None)
+        os.environ.pop("MAMBA_CLIP_AMD_FINE_STATES_MB", None)
+        if variant == "conc_text":
+            os.environ["MAMBA_CLIP_AMD_SIDE_TOWER"] = "text"
+        if variant.endswith("_nofine"):
+            os.environ["MAMBA_CLIP_AMD_FINE_STATES_MB"] = "0"
+        for m in model.modules():
+            if hasattr(m, "fused_attention"):
+                m.fused_attention = not variant.endswith("_noattn")
+        ops.WGRAD_HIP = variant.endswith("_wgradhip")
+        ops.WCAST_T = variant != "conc_nowt"
+        hip = train.HIP_ADAMW
+        train.HIP_ADAMW = variant != "conc_torchadam"
+        opt = train.create_optimizer(model, targs)
+        train.HIP_ADAMW = hip
+        rec = {}
+        losses = []
+        for s in range(args.steps):
+            opt.zero_grad(set_to_none=True)
+            with autocast():
+                out = model(images, texts)
+                if variant == "conc_sync":
+                    torch.cuda.synchronize()
+                total = loss_fn(**out)["contrastive_loss"]
+            total.backward()
+            if variant == "conc_sync":
+                torch.cuda.synchronize()
+            if s == 0:
+                rec["img_f"] = out["image_features"].detach().clone()
+                rec["txt_f"] = out["text_features"].detach().clone()
+                rec["grads"] = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+            losses.append(total.detach().clone())
+            train.optimizer_step(model, opt, None, targs)
+            del out, total
+        torch.cuda.synchronize()
+        rec["loss"] = [float(x) for x in losses]
+        rec["params"] = {n: p.detach().clone() for n, p in model.named_parameters()}
+        del opt
+        return rec
+
+    def diff(a, b):
+        d = {"img_f_equal": torch.equal(a["img_f"], b["img_f"]), "txt_f_equal": torch.equal(a["txt_f"], b["txt_f"]),
+             "loss": [x.hex() for x in b["loss"]], "loss_equal": a["loss"] == b["loss"]}
+        bad = [n for n in names if n in a["grads"] and not torch.equal(a["grads"][n], b["grads"][n])]
+        d["grads_differ"] = len(bad)
+        d["grads_differ_image"] = [n for n in bad if n in img_names][:6]
+        d["grads_differ_text"] = [n for n in bad if n not in img_names][:6]
+        d["grads_differ_last_img"] = [n for n in bad if n in img_names][-3:]
+        d["grads_differ_last_txt"] = [n for n in bad if n not in img_names][-3:]
+        pb = [n for n in names if not torch.equal(a["params"][n], b["params"][n])]
+        d["params_differ"] = len(pb)
+        if bad:
+            n = bad[0]
+            d["first_grad_maxdiff"] = float((a["grads"][n].float() - b["grads"][n].float()).abs().max())
+        return d
+
+    order = list(reversed(names))    # roughly backward order within each tower
+    ref = None
+    prev = {}
+    report = {"caching": os.environ.get("PYTORCH_NO_CUDA_MEMORY_CACHING", "") == "", "batch": args.batch,
+              "steps": args.steps, "runs": []}
+    for variant in args.variants.split(","):
+        for r in range(args.repeats):
+            t0 = time.time()
+            rec = run(variant)
+            base = ref if args.compare == "first" else prev.get(variant)
+            if base is None:
+                line = {"variant": variant, "repeat": r, "reference": True, "loss": [x.hex() for x in rec["loss"]]}
+            else:
+                line = {"variant": variant, "repeat": r, **diff(base, rec)}
+                bad = [n for n in order if n in base["grads"] and not torch.equal(base["grads"][n], rec["grads"][n])]
+                line["first_bad_grads_bwd_order"] = bad[:4]
+            nan = [n for n, g in rec["grads"].items() if not bool(torch.isfinite(g).all())]
+            if nan:
+                line["nonfinite_grads"] = nan[:6]
+            if ref is None:
+                ref = rec
+            prev[variant] = rec
+            line["s"] = round(time.time() - t0, 2)
+            report["runs"].append(line)
+            print(json.dumps(line), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(report, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -23,6 +23,13 @@ gemms = [r for r in seg if "Cijk_" in r["Kernel_Name"]]
 log = json.load(open(calls_path))
 calls = log["calls"]
 print(f"model {log['model']} batch {log['batch']} tuned {log['tuned']} env {log['env']}")
+# the run's tag names the grid mode it meant to measure (c*_default / c*_dp): flag a mismatch (the
+# package sets TENSILE_STREAMK_DATA_PARALLEL=1 at import when the variable is unset)
+_dp = log["env"].get("TENSILE_STREAMK_DATA_PARALLEL")
+if "_default" in calls_path and _dp != "0":
+    print(f"WARNING: default-grid leg ran with TENSILE_STREAMK_DATA_PARALLEL={_dp!r} (expected '0')")
+if "_dp" in calls_path and _dp != "1":
+    print(f"WARNING: data-parallel leg ran with TENSILE_STREAMK_DATA_PARALLEL={_dp!r} (expected '1')")
 print(f"{len(gemms)} GEMM dispatches in the step, {len(calls)} aten GEMM calls logged")
 
 TOWER = {}
