@@ -235,13 +235,266 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const Args g) {
     }
 }
 
+// ------------------------------------------------------------------ 4-phase-per-K-step pipeline
+// Same tile / waves / operand layouts as wgrad_kernel, but each 64-deep K step is split into four
+// phases of 16 MFMAs (one quadrant of a wave's 128 x 64 output: 64 x 32 over K 64), and the stage
+// is split into HALF-tiles by quadrant: A half qm = the rows {wr * 128 + qm * 64 + [0, 64)} of both
+// wave rows, B half qn = the columns {wc * 64 + qn * 32 + [0, 32)} of the four wave columns.  Each
+// half is read in known phases only, so it is restaged for the step after next as soon as its last
+// reader phase has retired its reads (a barrier later), one half-tile (two glds per thread) per phase:
+//   phase 1: read B qn0 + A qm0, MFMA (0, 0);  issue B half 0 of step t + 1   (last read: t - 1, phase 4)
+//   phase 2: read B qn1,         MFMA (0, 1);  issue A half 0 of step t + 2   (last read: t, phase 1)
+//   phase 3: read A qm1,         MFMA (1, 1);  issue B half 1 of step t + 2   (last read: t, phase 2)
+//   phase 4: read B qn0,         MFMA (1, 0);  issue A half 1 of step t + 2   (last read: t, phase 3)
+// and the only vmcnt wait is at phase 4: vmcnt(6) leaves phases 2-4's three half-tiles in flight and
+// retires everything step t + 1 needs.  Two LDS stages x 4 half-tiles x 16 KB = 128 KB.
+// (cdna_hip_programming.md section 5, "the 256^2 8-phase template": the same structure, one K step
+// per four phases.)
+constexpr int kHalf = 16 * 1024;     // one half-tile image (A or B, 128 features x 64 tokens)
+
+template <bool kFM, bool kIsA>
+__device__ __forceinline__ void half_sources(const char* base, int64_t ld, int dim, int f0, int h, int w, int lane,
+                                             const char* (&src)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pos = w * 2048 + j * 1024 + lane * 16;   // byte in the half image
+    int r, c, fl;                                       // image row, logical chunk, feature of the chunk / row
+    if constexpr (!kFM) {
+      r = pos >> 8;                                     // token row of 256 B = 16 chunks of 8 features
+      c = tm_slot(r, (pos >> 4) & 15);
+      fl = kIsA ? ((c >> 3) * 128 + h * 64 + (c & 7) * 8) : ((c >> 2) * 64 + h * 32 + (c & 3) * 8);
+      const int f = min(f0 + fl, dim - 8);
+      src[j] = base + ((int64_t)r * ld + f) * 2;
+    } else {
+      r = pos >> 7;                                     // feature row of 128 B = 8 chunks of 8 tokens
+      c = fm_slot(r, (pos >> 4) & 7);
+      fl = kIsA ? ((r >> 6) * 128 + h * 64 + (r & 63)) : ((r >> 5) * 64 + h * 32 + (r & 31));
+      const int f = min(f0 + fl, dim - 1);
+      src[j] = base + ((int64_t)f * ld + 8 * c) * 2;
+    }
+  }
+}
+
+// kStagger: the wave row wr = 1 runs one barrier behind wr = 0 (an extra s_barrier before the loop,
+// wr = 0 takes its extra one after it), so on every SIMD -- which holds one wave of each row -- one
+// wave's fragment reads overlap the other's MFMA cluster.  Each phase then retires its reads
+// (lgkmcnt(0)) BEFORE its first barrier: the half-tile restaged one phase later is only written after
+// that barrier, which both rows have passed with their reads of it done (cdna_hip_programming.md
+// section 5: "one barrier MORE when two wave groups run staggered").
+template <typename T, bool kAFM, bool kBFM, bool kStagger>
+__global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 4 * kHalf];   // [stage][A h0, A h1, B h0, B h1]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int nwg = tiles * g.splits;
+  const int bid0 = blockIdx.x, xcd = bid0 & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid0 >> 3);
+  const int split = lin / tiles, tile = lin % tiles;
+  const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+  const int k_begin = (int)(((int64_t)split * g.nk) / g.splits), k_end = (int)(((int64_t)(split + 1) * g.nk) / g.splits);
+  const int nk = k_end - k_begin;
+
+  // glds sources: [half][instr]
+  const char* srcA[2][2];
+  const char* srcB[2][2];
+  half_sources<kAFM, true>(g.A, g.lda, g.M, m0, 0, w, lane, srcA[0]);
+  half_sources<kAFM, true>(g.A, g.lda, g.M, m0, 1, w, lane, srcA[1]);
+  half_sources<kBFM, false>(g.B, g.ldb, g.N, n0, 0, w, lane, srcB[0]);
+  half_sources<kBFM, false>(g.B, g.ldb, g.N, n0, 1, w, lane, srcB[1]);
+  const int64_t stepA = kAFM ? (int64_t)kBK * 2 : (int64_t)kBK * g.lda * 2;
+  const int64_t stepB = kBFM ? (int64_t)kBK * 2 : (int64_t)kBK * g.ldb * 2;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)(lds) + 2048u * w);
+  // half-tile image index: 0 A h0, 1 A h1, 2 B h0, 3 B h1
+  auto issue = [&](int step, int img) __attribute__((always_inline)) {
+    const int ks = k_begin + step;
+    const uint32_t dst = lds0 + (uint32_t)(((step & 1) * 4 + img) * kHalf);
+    const char* const* s = img < 2 ? srcA[img] : srcB[img - 2];
+    const int64_t st = img < 2 ? stepA : stepB;
+    glds16(s[0] + st * ks, dst);
+    glds16(s[1] + st * ks, dst + 1024);
+  };
+
+  // fragment read offsets within a half image
+  const int fg = lane >> 4, fi = lane & 15, fq = fi >> 2, fp = fi & 3;
+  int offA[4], offB[2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int base = wr * 64 + mi * 16;                 // feature within the half
+    if constexpr (!kAFM) {
+      const int r = 8 * fg + fq;
+      offA[mi] = r * 256 + (tm_slot(r, base / 8 + (fp >> 1)) << 4) + 8 * (fp & 1);
+    } else {
+      offA[mi] = (base + fi) * 128;
+    }
+  }
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int base = wc * 32 + ni * 16;
+    if constexpr (!kBFM) {
+      const int r = 8 * fg + fq;
+      offB[ni] = r * 256 + (tm_slot(r, base / 8 + (fp >> 1)) << 4) + 8 * (fp & 1);
+    } else {
+      offB[ni] = (base + fi) * 128;
+    }
+  }
+  auto frag = [&](const char* img, int off, int row, int kk, auto is_fm) __attribute__((always_inline)) -> s16x8 {
+    if constexpr (!decltype(is_fm)::value) {
+      const lds_char* p = (const lds_char*)(img) + off + kk * 32 * 256;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 256));
+      return cat8(lo, hi);
+    } else {
+      return *reinterpret_cast<const s16x8*>(img + off + (fm_slot(row, fg + 4 * kk) << 4));
+    }
+  };
+  auto read_a = [&](const char* img, s16x8 (&af)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[mi][kk] = frag(img, offA[mi], wr * 64 + mi * 16 + fi, kk, std::integral_constant<bool, kAFM>());
+  };
+  auto read_b = [&](const char* img, s16x8 (&bf)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bf[ni][kk] = frag(img, offB[ni], wc * 32 + ni * 16 + fi, kk, std::integral_constant<bool, kBFM>());
+  };
+
+  f32x4 acc[2][2][4][2];   // [qm][qn][mi][ni]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma_q = [&](int qm, int qn, const s16x8 (&af)[4][2], const s16x8 (&bf)[2][2]) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[qm][qn][mi][ni] = mfma<T>(af[mi][kk], bf[ni][kk], acc[qm][qn][mi][ni]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_reads = [&]() __attribute__((always_inline)) {
+    if constexpr (kStagger) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) first: the reads are retired before the barrier
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this phase's fragment reads are in
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: step 0 whole, step 1's A h0 / B h1 / A h1 (phases 2-4 of step -1); step 0 ready
+  if (nk > 0) {
+#pragma unroll
+    for (int img = 0; img < 4; ++img) issue(0, img);
+  }
+  if (nk > 1) {
+    issue(1, 0);
+    issue(1, 3);
+    issue(1, 1);
+    __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): step 0's eight loads done
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+  __builtin_amdgcn_s_barrier();
+
+  s16x8 af[4][2], bf0[2][2], bf1[2][2];
+  if (kStagger && wr == 1) __builtin_amdgcn_s_barrier();   // wr is wave-uniform (readfirstlane'd w)
+  for (int t = 0; t < nk; ++t) {
+    const char* st = lds + (t & 1) * 4 * kHalf;
+    // ---- phase 1: B qn0 + A qm0 -> quadrant (0, 0); stage B h0 of step t + 1
+    read_b(st + 2 * kHalf, bf0);
+    read_a(st + 0 * kHalf, af);
+    if (t + 1 < nk) issue(t + 1, 2);
+    sync_reads();
+    mma_q(0, 0, af, bf0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: B qn1 -> (0, 1); stage A h0 of step t + 2
+    read_b(st + 3 * kHalf, bf1);
+    if (t + 2 < nk) issue(t + 2, 0);
+    sync_reads();
+    mma_q(0, 1, af, bf1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 3: A qm1 -> (1, 1); stage B h1 of step t + 2
+    read_a(st + 1 * kHalf, af);
+    if (t + 2 < nk) issue(t + 2, 3);
+    sync_reads();
+    mma_q(1, 1, af, bf1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 4: B qn0 (re-read) -> (1, 0); stage A h1 of step t + 2; step t + 1 retired
+    read_b(st + 2 * kHalf, bf0);
+    if (t + 2 < nk) {
+      issue(t + 2, 1);
+      __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): all but step t + 2's three half-tiles
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // tail: nothing of a later step in flight
+    }
+    sync_reads();
+    mma_q(1, 0, af, bf0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (kStagger && wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both rows
+
+  // ---- epilogue: quadrant (qm, qn), tile (mi, ni): rows wr*128 + qm*64 + mi*16 + 4 (l >> 4) + r,
+  // column wc*64 + qn*32 + ni*16 + (l & 15)
+  float* C = g.C + (int64_t)split * g.slab_stride;
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int col = n0 + wc * 64 + qn * 32 + ni * 16 + fi;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wr * 128 + qm * 64 + mi * 16 + 4 * fg + r;
+            if (row < g.M && col < g.N) C[(int64_t)row * g.ldc + col] = acc[qm][qn][mi][ni][r];
+          }
+        }
+}
+
+// MC_WGRAD_PIPE: 5 = four-phase pipeline with staggered wave rows (default), 4 = four-phase, rows in
+// step, 2 = wgrad_kernel (two barriers per K step)
+static int wgrad_pipe() {   // read per call: A/B runs flip it inside one process
+  const char* e = getenv("MC_WGRAD_PIPE");
+  return e ? atoi(e) : 5;
+}
+
 template <typename T>
 static void launch_t(const Args& a, bool afm, bool bfm, hipStream_t s) {
   const dim3 grid(a.tiles_m * a.tiles_n * a.splits), block(kThreads);
-  if (!afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, false>), grid, block, 0, s, a);
-  else if (!afm && bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, true>), grid, block, 0, s, a);
-  else if (afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, true, false>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((wgrad_kernel<T, true, true>), grid, block, 0, s, a);
+  if (wgrad_pipe() == 2) {
+    if (!afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, false>), grid, block, 0, s, a);
+    else if (!afm && bfm) hipLaunchKernelGGL((wgrad_kernel<T, false, true>), grid, block, 0, s, a);
+    else if (afm && !bfm) hipLaunchKernelGGL((wgrad_kernel<T, true, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, true, true>), grid, block, 0, s, a);
+    return;
+  }
+  if (wgrad_pipe() == 4) {
+    if (!afm && !bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, false, false, false>), grid, block, 0, s, a);
+    else if (!afm && bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, false, true, false>), grid, block, 0, s, a);
+    else if (afm && !bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, true, false, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, false>), grid, block, 0, s, a);
+    return;
+  }
+  if (!afm && !bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, false, false, true>), grid, block, 0, s, a);
+  else if (!afm && bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, false, true, true>), grid, block, 0, s, a);
+  else if (afm && !bfm) hipLaunchKernelGGL((wgrad4p_kernel<T, true, false, true>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true>), grid, block, 0, s, a);
 }
 
 static int auto_splits(int tiles, int nk) {

@@ -21,6 +21,7 @@ add+RMSNorm / add+LayerNorm, patch im2col, short-sequence attention
 (attention.hip), contrastive loss; dense projections are plain library GEMMs
 (hipBLASLt through torch, launched data-parallel: see __init__.py).
 """
+import contextlib
 import math
 import os
 from functools import partial
@@ -476,6 +477,30 @@ class ClipModel(nn.Module):
             return None
         return self.side_stream_for(image.device)
 
+    def _towers_two_streams(self, image, text, side, main, dt=None):
+        """(image_features, text_features) with the side tower on `side`.  With dt, each tower runs in its own
+        weight-cast scope entered on its own stream; without (shared_weight_casts), the caller's scope
+        serves both."""
+        def scope(module):
+            return weight_cast_scope(module, dt) if dt is not None else contextlib.nullcontext()
+        if self.side_tower == "image":
+            image.record_stream(side)
+            with torch.cuda.stream(side), scope(self.visual):
+                image_features = self.encode_image(image, normalize=True)
+            with scope(self.text):
+                text_features = self.encode_text(text, normalize=True)
+            main.wait_stream(side)
+            image_features.record_stream(main)
+        else:
+            text.record_stream(side)
+            with torch.cuda.stream(side), scope(self.text):
+                text_features = self.encode_text(text, normalize=True)
+            with scope(self.visual):
+                image_features = self.encode_image(image, normalize=True)
+            main.wait_stream(side)
+            text_features.record_stream(main)
+        return image_features, text_features
+
     def encode_image(self, image, normalize: bool = False):
         f = self.visual(image)
         return F.normalize(f, dim=-1) if normalize else f
@@ -484,38 +509,45 @@ class ClipModel(nn.Module):
         f = self.text(text)
         return F.normalize(f, dim=-1) if normalize else f
 
+    # A/B switch (round 4 behaviour): one weight-cast buffer for both towers, made on the main stream and
+    # handed to the side stream with record_stream.  Off: each tower casts its own weights on its own stream
+    # (DESIGN 4.9), so no buffer crosses the streams in either direction.
+    shared_weight_casts = os.environ.get("MAMBA_CLIP_AMD_SHARED_WEIGHT_CASTS", "0") == "1"
+
     def forward(self, image, text, secondary_text=None):
-        # under CUDA autocast: the towers' Linear weights cast to 16 bits in one launch for this
-        # forward (ops.weight_cast_scope) instead of one cast per weight and use
+        # under CUDA autocast: the towers' Linear weights cast to 16 bits in one launch per tower and forward
+        # (ops.weight_cast_scope) instead of one cast per weight and use
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
-        with weight_cast_scope(self, dt) as casts:
-            side = self._side_stream(image, text)
-            if side is None:
+        side = self._side_stream(image, text)
+        secondary = None
+        if side is None:
+            with weight_cast_scope(self, dt):
                 image_features = self.encode_image(image, normalize=True) if image is not None else None
                 text_features = self.encode_text(text, normalize=True) if text is not None else None
-            else:
-                # the towers are independent until the loss: the text tower runs on a second HIP stream
-                # beside the image tower (its backward follows it there: autograd runs each backward op
-                # on its forward op's stream and joins the streams at the end of backward)
+                if secondary_text is not None:
+                    secondary = self.encode_text(secondary_text, normalize=True)
+        elif self.shared_weight_casts:
+            with weight_cast_scope(self, dt) as casts:
                 main = torch.cuda.current_stream()
-                self.last_main_stream = main                 # train._join_streams_allreduce joins it
-                side.wait_stream(main)                       # the one-launch weight casts, the inputs
+                self.last_main_stream = main
+                side.wait_stream(main)
                 casts.record_stream(side)
-                if self.side_tower == "image":
-                    image.record_stream(side)
-                    with torch.cuda.stream(side):
-                        image_features = self.encode_image(image, normalize=True)
-                    text_features = self.encode_text(text, normalize=True)
-                    main.wait_stream(side)
-                    image_features.record_stream(main)
-                else:
-                    text.record_stream(side)
-                    with torch.cuda.stream(side):
-                        text_features = self.encode_text(text, normalize=True)
-                    image_features = self.encode_image(image, normalize=True)
-                    main.wait_stream(side)
-                    text_features.record_stream(main)
-            secondary = self.encode_text(secondary_text, normalize=True) if secondary_text is not None else None
+                image_features, text_features = self._towers_two_streams(image, text, side, main)
+                if secondary_text is not None:
+                    secondary = self.encode_text(secondary_text, normalize=True)
+        else:
+            # the towers are independent until the loss: one of them runs on a second HIP stream (its
+            # backward follows it there: autograd runs each backward op on its forward op's stream and joins
+            # the streams at the end of backward).  Each tower's weight casts are made on the stream that
+            # uses them, so nothing allocated on one stream is read on the other except the inputs (recorded)
+            # and the side tower's features (recorded for the loss on the main stream).
+            main = torch.cuda.current_stream()
+            self.last_main_stream = main                 # train._join_streams_allreduce joins it
+            side.wait_stream(main)                       # the inputs, the parameters the optimizer updated
+            image_features, text_features = self._towers_two_streams(image, text, side, main, dt)
+            if secondary_text is not None:
+                with weight_cast_scope(self.text, dt):
+                    secondary = self.encode_text(secondary_text, normalize=True)
         if self.output_dict:
             out = {"image_features": image_features, "text_features": text_features,
                    "logit_scale": self.logit_scale.exp()}

@@ -120,7 +120,10 @@ def wrap_ddp(model, args, device):
               bucket_cap_mb=getattr(args, "ddp_bucket_mb", 100))
     if device.type == "cuda":
         kw["device_ids"] = [device]
-    side = model.side_stream_for(device) if (device.type == "cuda" and hasattr(model, "side_stream_for")) else None
+    # MAMBA_CLIP_AMD_DDP_SIDE_STREAM=0 keeps the towers on one stream under DDP (the two-stream comm hook
+    # below is covered by gloo tests; ADVICE r04 asks for a switch until an RCCL run has covered it)
+    two = os.environ.get("MAMBA_CLIP_AMD_DDP_SIDE_STREAM", "1") != "0"
+    side = model.side_stream_for(device) if (two and device.type == "cuda" and hasattr(model, "side_stream_for")) else None
     if side is not None and hasattr(model, "side_tower_module"):
         # DDP keeps every parameter's AccumulateGrad node alive from here on, and a node runs on the
         # stream current at its creation.  Created now on the main stream, each text-tower gradient
@@ -261,10 +264,17 @@ class GraphedStep:
         return lambda: torch.autocast("cuda", dtype=dt, cache_enabled=False)
 
     def __init__(self, model, images, texts, targets, loss, optimizer, args, warmup=3):
+        if getattr(args, "balanced_mixup", None):
+            # the mixup draws lam (and the lam > 0.5 text swap) on the host: a replay would repeat the
+            # capture's draw forever
+            raise ValueError("GraphedStep: balanced_mixup draws host-side randomness per step; run it eager")
         autocast = self.autocast_for(args)
+        inner = unwrap_model(model)
         # one stream: the towers' two-stream fork / join does not survive capture race-free here (replays
-        # of a two-stream capture differed run to run in round 4's test); replay order = eager order
-        unwrap_model(model).concurrent_towers = False
+        # of a two-stream capture differed run to run in round 4's test); replay order = eager order.
+        # The flag is restored after the capture, so later eager steps run the towers concurrently again.
+        prev = getattr(inner, "concurrent_towers", False)
+        inner.concurrent_towers = False
         run = lambda: train_step(model, images, texts, targets, loss, optimizer, None, args, autocast)  # noqa: E731
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -275,8 +285,12 @@ class GraphedStep:
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         optimizer.zero_grad(set_to_none=True)     # gradients are allocated inside the capture's pool
-        with torch.cuda.graph(self.graph):
-            self.losses = run()
+        try:
+            with torch.cuda.graph(self.graph):
+                self.losses = run()
+        finally:
+            if hasattr(inner, "concurrent_towers"):
+                inner.concurrent_towers = prev
 
     def __call__(self):
         self.graph.replay()

@@ -40,10 +40,13 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("pipe", ["5", "4", "2"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"N{c[0]}K{c[1]}T{c[2]}{'F' if c[3] else 'T'}{'F' if c[4] else 'T'}")
-def test_wgrad_matches_fp64(case, dt):
+def test_wgrad_matches_fp64(case, dt, pipe, monkeypatch):
+    """Every main-loop variant (MC_WGRAD_PIPE: 5 staggered four-phase, 4 four-phase, 2 two-barrier)."""
     from mamba_clip_amd.ops import wgrad_hip
+    monkeypatch.setenv("MC_WGRAD_PIPE", pipe)
     N, K, T, a_fm, b_fm = case
     G, X = _operands(N, K, T, dt, a_fm, b_fm, seed=N + K)
     out = wgrad_hip(G, X)

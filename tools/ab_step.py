@@ -1,7 +1,8 @@
 """Dev tool: interleaved same-box A/B of the C2 training step with a model toggle (not the bench contract).
 
 usage: python tools/ab_step.py --toggle fuse_dt_proj [--model vit_b16-mamba130m --batch 256 --steps 10 --reps 3]
-The toggle is an attribute set on every text-mixer module (True = variant A, False = variant B).
+The toggle is an attribute set on every module that has it (True = variant A, False = variant B), or
+`ops.NAME` / `train.NAME` for a module-level flag of mamba_clip_amd.ops / .train.
 """
 import argparse
 import os
@@ -41,13 +42,20 @@ opt = create_optimizer(model, targs)
 loss = ClipLoss()
 images, texts, targets = synthetic_batch(args.batch, 224, model.text.context_length, model.text.vocab_size,
                                          device=dev, seed=1000)
-mods = [m for m in model.modules() if hasattr(m, args.toggle)]
-print(f"{len(mods)} modules carry {args.toggle}")
+if args.toggle.startswith(("ops.", "train.")):
+    import importlib
+    modname, attr = args.toggle.split(".", 1)
+    holder = importlib.import_module(f"mamba_clip_amd.{modname}")
+    mods, tog = [holder], attr
+else:
+    mods = [m for m in model.modules() if hasattr(m, args.toggle)]
+    tog = args.toggle
+print(f"{len(mods)} holders carry {args.toggle}")
 
 
 def run(flag, steps):
     for m in mods:
-        setattr(m, args.toggle, flag)
+        setattr(m, tog, flag)
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(steps):

@@ -84,6 +84,7 @@ def main():
                 m.fused_attention = not variant.endswith("_noattn")
         ops.WGRAD_HIP = variant.endswith("_wgradhip")
         ops.WCAST_T = variant != "conc_nowt"
+        ClipModel.shared_weight_casts = variant.endswith("_sharedcast")
         hip = train.HIP_ADAMW
         train.HIP_ADAMW = variant != "conc_torchadam"
         opt = train.create_optimizer(model, targs)

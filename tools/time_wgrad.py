@@ -65,7 +65,12 @@ def main():
         ops.WGRAD_HIP = False
         lib_us = timed(lambda: ops.wgrad(G, X))
         ref = ops.wgrad(G, X)
-        hip_us = timed(lambda: ops.wgrad_hip(G, X))
+        pipes = {}
+        for pipe in ("2", "4", "5"):
+            os.environ["MC_WGRAD_PIPE"] = pipe
+            pipes[pipe] = round(timed(lambda: ops.wgrad_hip(G, X)), 1)
+        os.environ["MC_WGRAD_PIPE"] = "5"
+        hip_us = pipes["5"]
         out = ops.wgrad_hip(G, X)
         err = float((out - ref).abs().max() / ref.abs().max())
         sweep = {}
@@ -74,7 +79,8 @@ def main():
                 sweep[s] = round(timed(lambda: ops.wgrad_hip(G, X, splits=s), iters=10, rounds=3), 1)
         print(json.dumps({"shape": name, "N": N, "K": K, "T": T, "lib_us": round(lib_us, 1), "hip_us": round(hip_us, 1),
                           "lib_tflops": round(flop / lib_us / 1e6, 1), "hip_tflops": round(flop / hip_us / 1e6, 1),
-                          "rel_err_vs_lib": err, "hip_split_sweep_us": sweep}), flush=True)
+                          "rel_err_vs_lib": err, "pipe_us": pipes,
+                          "hip_split_sweep_us": sweep}), flush=True)
 
 
 if __name__ == "__main__":
