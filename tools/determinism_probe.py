@@ -11,6 +11,7 @@ Variants (comma list, --variants):
   conc      towers on two streams (the default path)
   seq       one stream
   conc_sync two streams, device synchronize after forward and after backward
+  conc_fsync two streams, device synchronize after forward only
   conc_torchadam  two streams, torch's fused AdamW instead of HipAdamW
   conc_text two streams, text tower on the side stream
   conc_nowt two streams, no transposed weight copies (ops.WCAST_T off)
@@ -39,6 +40,11 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--compare", choices=["first", "prev"], default="first",
                     help="compare each run with the first run overall, or with the previous run of its variant")
+    ap.add_argument("--summary", action="store_true",
+                    help="compare every run with one seq run: per variant, how many of --repeats runs differ "
+                         "(step-1 grads, final params, losses) and their first differing grads in backward order")
+    ap.add_argument("--self-ref", action="store_true",
+                    help="with --summary: compare each variant's runs with an extra first run of that variant")
     ap.add_argument("--fill-nan", action="store_true",
                     help="torch.use_deterministic_algorithms(warn_only) + fill_uninitialized_memory: every torch.empty "
                          "is NaN-filled, so a kernel reading memory it never wrote shows up")
@@ -75,7 +81,7 @@ def main():
         model.concurrent_towers = not variant.startswith("seq")
         os.environ.pop("MAMBA_CLIP_AMD_SIDE_TOWER", None)
         os.environ.pop("MAMBA_CLIP_AMD_FINE_STATES_MB", None)
-        if variant == "conc_text":
+        if variant.startswith("conc_text"):
             os.environ["MAMBA_CLIP_AMD_SIDE_TOWER"] = "text"
         if variant.endswith("_nofine"):
             os.environ["MAMBA_CLIP_AMD_FINE_STATES_MB"] = "0"
@@ -91,12 +97,17 @@ def main():
         train.HIP_ADAMW = hip
         rec = {}
         losses = []
+        from mamba_clip_amd import selective_scan_interface as ssi
+        rec["fine_live_mb"] = []
         for s in range(args.steps):
             opt.zero_grad(set_to_none=True)
+            live0 = ssi.fine_states_live_bytes()
             with autocast():
                 out = model(images, texts)
-                if variant == "conc_sync":
-                    torch.cuda.synchronize()
+            rec["fine_live_mb"].append((live0 >> 20, ssi.fine_states_live_bytes() >> 20))
+            if variant in ("conc_sync", "conc_fsync"):
+                torch.cuda.synchronize()
+            with autocast():
                 total = loss_fn(**out)["contrastive_loss"]
             total.backward()
             if variant == "conc_sync":
@@ -131,6 +142,32 @@ def main():
         return d
 
     order = list(reversed(names))    # roughly backward order within each tower
+    if args.summary:
+        ref = run("seq")
+        summ = {}
+        for variant in args.variants.split(","):
+            bad_runs, firsts, t0 = 0, {}, time.time()
+            if args.self_ref:
+                run(variant)            # warm-up: a variant switch rebuilds plans / registrations on its first run
+                ref = run(variant)
+            for r in range(args.repeats):
+                rec = run(variant)
+                bad = [n for n in order if not torch.equal(ref["grads"][n], rec["grads"][n])]
+                pbad = sum(1 for n in names if not torch.equal(ref["params"][n], rec["params"][n]))
+                if bad or pbad or rec["loss"] != ref["loss"]:
+                    print(json.dumps({"variant": variant, "repeat": r, "fine_live_mb": rec["fine_live_mb"],
+                                      "ref_fine_live_mb": ref["fine_live_mb"], "first_bad": bad[:2]}), flush=True)
+                    bad_runs += 1
+                    key = ",".join(bad[:2]) if bad else "params-only"
+                    firsts[key] = firsts.get(key, 0) + 1
+            summ[variant] = {"runs": args.repeats, "runs_differ": bad_runs, "first_bad": firsts,
+                             "s": round(time.time() - t0, 1)}
+            print(json.dumps({"variant": variant, **summ[variant]}), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump({"caching": os.environ.get("PYTORCH_NO_CUDA_MEMORY_CACHING", "") == "",
+                           "batch": args.batch, "steps": args.steps, "summary": summ}, f, indent=1)
+        return
     ref = None
     prev = {}
     report = {"caching": os.environ.get("PYTORCH_NO_CUDA_MEMORY_CACHING", "") == "", "batch": args.batch,
