@@ -236,6 +236,29 @@ typedef struct mc_mixer_proj_bwd_params {
 
 int mc_mixer_proj_bwd(const mc_mixer_proj_bwd_params* p, void* stream);
 
+/* mc_colsum: out[c] = sum_{r < rows} x[r * ld + c] in fp32, c < cols, x fp32 / bf16 / fp16 row-major
+ * (row stride ld elements).  Fixed row slices summed per workgroup, the slice partials folded in order:
+ * deterministic, and no workgroup reads another's results during the launch.  Replaces torch's batch /
+ * token reductions in the towers' glue -- the bias gradients of projections whose producer left no
+ * column sums (ops.LinearSK), the ViT's cls_token / pos_embed and BERT's position gradients -- whose
+ * cross-workgroup combine returned wrong sums beside concurrent library GEMMs.
+ * Reference: the autograd reductions behind model.py:232-358's token embedding (open_clip / timm
+ * VisionTransformer._pos_embed).  16-B vector loads when ld, cols and x allow.  Workspace:
+ * mc_colsum_workspace_bytes(rows, cols). */
+size_t mc_colsum_workspace_bytes(int32_t rows, int32_t cols);
+int mc_colsum(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ld, float* out,
+              void* workspace, size_t workspace_bytes, void* stream);
+
+/* mc_l2norm_fwd / _bwd: torch.nn.functional.normalize(x, dim=-1) for a (rows, cols) matrix -- the
+ * features ClipModel.encode_image / encode_text(normalize=True) return (reference model.py:1011-1017).
+ * Forward y = x / max(||x||, eps) in fp32, norm[r] = ||x_r||; backward dx = (g - y (y . g)) / ||x||
+ * (g / eps where the clamp is active), dx in x's dtype.  One wave per row: no cross-workgroup
+ * reduction (torch's norm launch splits each row over 8 workgroups). */
+int mc_l2norm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ldx, float eps,
+                  float* y, int64_t ldy, float* norm, void* stream);
+int mc_l2norm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ldx, const float* norm,
+                  float eps, const float* g, int64_t ldg, void* dx, int64_t lddx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

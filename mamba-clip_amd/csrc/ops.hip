@@ -929,6 +929,106 @@ __global__ __launch_bounds__(256) void colsum_slices_kernel(const float* __restr
   }
 }
 
+
+// ------------------------------------------------------------------ column sums and row L2-normalize
+// The reductions the towers' glue would otherwise leave to torch: torch's cross-
+// workgroup reductions (a staging buffer and a per-output ticket combine partials from several
+// workgroups) returned wrong sums for ~0.1 % of the outputs while library GEMMs ran on the other
+// stream (tools/sum_under_load.py).  These kernels never hand data between workgroups of one launch:
+// pass 1 writes one partial row per fixed row slice, pass 2 (colsum_slices_kernel) folds the slices
+// in order -- deterministic and independent of what else runs on the device.
+
+// part[slice][c] = sum over rows [slice * per, (slice + 1) * per) of x[r][c]; block = 4 row lanes x 64
+// column vectors of V elements, the 4 lanes meet in LDS in a fixed order.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void colsum_rows_kernel(int rows, int cols, const T* __restrict__ x, int64_t ld,
+                                                          float* __restrict__ part) {
+  __shared__ float red[3][64 * V];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cv = blockIdx.x * 64 + lane;
+  const bool ok = cv * V < cols;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (ok) {
+    if constexpr (V > 1) {
+#pragma unroll 4
+      for (int r = r0 + rl; r < r1; r += 4) {
+        const uint4 q = ld16(x + (int64_t)r * ld + cv * V);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += elem_f<T>(q, e);
+      }
+    } else {
+#pragma unroll 4
+      for (int r = r0 + rl; r < r1; r += 4) acc[0] += to_f(x[(int64_t)r * ld + cv]);
+    }
+  }
+  if (rl > 0) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[rl - 1][lane * V + e] = acc[e];
+  }
+  __syncthreads();
+  if (rl == 0 && ok) {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      part[(int64_t)blockIdx.y * cols + cv * V + e] = ((acc[e] + red[0][lane * V + e]) + red[1][lane * V + e]) +
+                                                      red[2][lane * V + e];
+  }
+}
+
+// y = x / max(||x||, eps) per row (torch.nn.functional.normalize, p = 2); one wave per row, fp32 out,
+// norm[r] = ||x_r|| (unclamped) saved for the backward.
+template <typename T>
+__global__ __launch_bounds__(256) void l2norm_fwd_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
+                                                         float eps, float* __restrict__ y, int64_t ldy,
+                                                         float* __restrict__ norm) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const T* xr = x + (int64_t)r * ldx;
+  float ss = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float v = to_f(xr[c]);
+    ss += v * v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  const float n = sqrtf(ss);
+  const float inv = 1.f / fmaxf(n, eps);
+  float* yr = y + (int64_t)r * ldy;
+  for (int c = lane; c < cols; c += 64) yr[c] = to_f(xr[c]) * inv;
+  if (lane == 0) norm[r] = n;
+}
+
+// dx = (g - y (y . g)) / ||x|| where ||x|| > eps, else g / eps (the clamp passes no gradient to the
+// norm); y recomputed from x.  dx in x's dtype.
+template <typename T>
+__global__ __launch_bounds__(256) void l2norm_bwd_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
+                                                         const float* __restrict__ norm, float eps,
+                                                         const float* __restrict__ g, int64_t ldg,
+                                                         T* __restrict__ dx, int64_t lddx) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const T* xr = x + (int64_t)r * ldx;
+  const float* gr = g + (int64_t)r * ldg;
+  const float n = norm[r];
+  const bool clamped = !(n > eps);
+  const float c_ = clamped ? eps : n;
+  float dot = 0.f;
+  if (!clamped) {
+    for (int c = lane; c < cols; c += 64) dot += to_f(xr[c]) * gr[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  }
+  const float inv = 1.f / c_;
+  const float k = clamped ? 0.f : dot * inv * inv * inv;   // (y . g) / c with y = x / c
+  T* dr = dx + (int64_t)r * lddx;
+  for (int c = lane; c < cols; c += 64) dr[c] = from_f<T>(gr[c] * inv - to_f(xr[c]) * k);
+}
+
 }  // namespace mc
 
 using namespace mc;
@@ -1433,4 +1533,65 @@ extern "C" int mc_sum_slabs(int32_t s, int64_t n, const float* src, int64_t slab
   if (vec) hipLaunchKernelGGL(sum_slabs_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, s, n, src, slab_stride, dst);
   else hipLaunchKernelGGL(sum_slabs_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, s, n, src, slab_stride, dst);
   return check_launch("mc_sum_slabs");
+}
+
+// ------------------------------------------------------------------ column sums, row L2-normalize (C-ABI)
+static int colsum_slices(int rows) { return std::max(1, std::min(kGradSlices, (rows + 31) / 32)); }
+
+extern "C" size_t mc_colsum_workspace_bytes(int32_t rows, int32_t cols) {
+  return (size_t)colsum_slices(std::max(rows, 0)) * (size_t)std::max(cols, 0) * sizeof(float);
+}
+
+extern "C" int mc_colsum(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ld, float* out,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_colsum: bad dtype");
+  MC_CHECK(rows >= 0 && cols >= 0 && ld >= cols, MC_ERR_SHAPE, "mc_colsum: bad shape (rows %d, cols %d, ld %lld)",
+           rows, cols, (long long)ld);
+  hipStream_t s = (hipStream_t)stream;
+  if (cols == 0) return MC_OK;
+  MC_CHECK(out, MC_ERR_INVALID, "mc_colsum: null output");
+  if (rows == 0) {
+    (void)hipMemsetAsync(out, 0, (size_t)cols * 4, s);
+    return check_launch("mc_colsum");
+  }
+  MC_CHECK(x && workspace && workspace_bytes >= mc_colsum_workspace_bytes(rows, cols), MC_ERR_WORKSPACE,
+           "mc_colsum: x and a workspace of mc_colsum_workspace_bytes required");
+  float* part = reinterpret_cast<float*>(workspace);
+  const int ns = colsum_slices(rows);
+  const int V = dtype == MC_DTYPE_F32 ? 4 : 8;
+  const bool vec = cols % V == 0 && ld % V == 0 && aligned16(x);
+  MC_DISPATCH_T(dtype, {
+    if (vec)
+      hipLaunchKernelGGL((colsum_rows_kernel<T, ElemTraits<T>::kVec>), dim3((unsigned)((cols / V + 63) / 64), ns),
+                         dim3(256), 0, s, rows, cols, (const T*)x, ld, part);
+    else
+      hipLaunchKernelGGL((colsum_rows_kernel<T, 1>), dim3((unsigned)((cols + 63) / 64), ns), dim3(256), 0, s, rows,
+                         cols, (const T*)x, ld, part);
+  });
+  hipLaunchKernelGGL(colsum_slices_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, part, ns, cols, out);
+  return check_launch("mc_colsum");
+}
+
+extern "C" int mc_l2norm_fwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ldx, float eps,
+                             float* y, int64_t ldy, float* norm, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_l2norm_fwd: bad dtype");
+  MC_CHECK(rows >= 0 && cols > 0 && ldx >= cols && ldy >= cols, MC_ERR_SHAPE, "mc_l2norm_fwd: bad shape");
+  if (rows == 0) return MC_OK;
+  MC_CHECK(x && y && norm, MC_ERR_INVALID, "mc_l2norm_fwd: x, y, norm required");
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((l2norm_fwd_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0,
+                                          (hipStream_t)stream, rows, cols, (const T*)x, ldx, eps, y, ldy, norm));
+  return check_launch("mc_l2norm_fwd");
+}
+
+extern "C" int mc_l2norm_bwd(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ldx, const float* norm,
+                             float eps, const float* g, int64_t ldg, void* dx, int64_t lddx, void* stream) {
+  MC_CHECK(dtype >= MC_DTYPE_F32 && dtype <= MC_DTYPE_F16, MC_ERR_DTYPE, "mc_l2norm_bwd: bad dtype");
+  MC_CHECK(rows >= 0 && cols > 0 && ldx >= cols && ldg >= cols && lddx >= cols, MC_ERR_SHAPE,
+           "mc_l2norm_bwd: bad shape");
+  if (rows == 0) return MC_OK;
+  MC_CHECK(x && norm && g && dx, MC_ERR_INVALID, "mc_l2norm_bwd: x, norm, g, dx required");
+  MC_DISPATCH_T(dtype, hipLaunchKernelGGL((l2norm_bwd_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0,
+                                          (hipStream_t)stream, rows, cols, (const T*)x, ldx, norm, eps, g, ldg,
+                                          (T*)dx, lddx));
+  return check_launch("mc_l2norm_bwd");
 }

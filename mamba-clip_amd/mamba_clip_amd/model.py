@@ -32,10 +32,10 @@ import torch.nn.functional as F
 import torch.utils.checkpoint
 
 from . import GEMM_GRIDS_DATA_PARALLEL
-from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_rmsnorm, attn_supported, causal_conv1d,
-                  fc1_gelu, linear_sk, mixer_proj, mixer_proj_ok, neg_exp_many, packed_attention, patch_im2col, qkv_proj, split_rows,
-                  split_rows_n,
-                  ss2d_conv_stack, ss2d_merge_ln_gate, weight_cast_scope, wleft_mm)
+from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_pos, add_rmsnorm, attn_supported,
+                  causal_conv1d, fc1_gelu, l2_normalize, linear_sk, mixer_proj, mixer_proj_ok, neg_exp_many,
+                  packed_attention, patch_im2col, qkv_proj, split_rows, split_rows_n, ss2d_conv_stack,
+                  ss2d_merge_ln_gate, token_embed, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
@@ -340,8 +340,8 @@ class VisionTransformer(nn.Module):
 
     def forward(self, x):
         x = self.patch_embed(x)
-        cls = self.cls_token.to(x.dtype).expand(x.shape[0], -1, -1)
-        m, h = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype), None
+        # cat([cls, x]) + pos with a deterministic backward (ops.TokenEmbedFn)
+        m, h = token_embed(self.cls_token, x, self.pos_embed), None
         m, h = _run_blocks(self.blocks, m, h, self.grad_checkpointing and torch.is_grad_enabled())
         # final norm on the pooled (cls) rows only: same values as norm(x)[:, 0]
         y, _ = add_layernorm(m[:, 0], h[:, 0], self.norm.weight, self.norm.bias, self.norm.eps)
@@ -385,7 +385,7 @@ class BertTextEncoder(nn.Module):
         self.grad_checkpointing = bool(enable)
 
     def forward(self, tokens):
-        m, h = self.ln(self.tok(tokens) + self.pos[:, : tokens.shape[1]]), None
+        m, h = self.ln(add_pos(self.tok(tokens), self.pos)), None
         m, h = _run_blocks(self.blocks, m, h, self.grad_checkpointing and torch.is_grad_enabled())
         return self.proj(m[:, 0] + h[:, 0])
 
@@ -442,13 +442,16 @@ class ClipModel(nn.Module):
 
     @property
     def side_tower(self):
-        """Which tower runs on the side stream: the image tower beside the Mamba text tower (C2 69.2 ->
-        68.9 ms per step), the text tower beside BERT; MAMBA_CLIP_AMD_SIDE_TOWER=text/image overrides (A/B;
-        profiles/r04/stream_priority/)."""
+        """Which tower runs on the side stream: the text tower, for every text tower.  Round 4 put the
+        image tower there beside the Mamba text tower (C2 -0.3 ms, profiles/r04/stream_priority/), but
+        that arrangement is not run-to-run reproducible: the Mamba tower's step-1 gradients differ from
+        run to run (10 distinct outcomes in 12, from the first scan backward on) while the text-on-side
+        arrangement repeats bitwise (profiles/r05/determinism/).  MAMBA_CLIP_AMD_SIDE_TOWER=
+        image restores it for A/B."""
         env = os.environ.get("MAMBA_CLIP_AMD_SIDE_TOWER")
         if env in ("text", "image"):
             return env
-        return "text" if isinstance(self.text, BertTextEncoder) else "image"
+        return "text"
 
     def side_tower_module(self):
         return self.visual if self.side_tower == "image" else self.text
@@ -503,11 +506,11 @@ class ClipModel(nn.Module):
 
     def encode_image(self, image, normalize: bool = False):
         f = self.visual(image)
-        return F.normalize(f, dim=-1) if normalize else f
+        return l2_normalize(f) if normalize else f
 
     def encode_text(self, text, normalize: bool = False):
         f = self.text(text)
-        return F.normalize(f, dim=-1) if normalize else f
+        return l2_normalize(f) if normalize else f
 
     # A/B switch (round 4 behaviour): one weight-cast buffer for both towers, made on the main stream and
     # handed to the side stream with record_stream.  Off: each tower casts its own weights on its own stream

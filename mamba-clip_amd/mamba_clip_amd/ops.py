@@ -734,6 +734,114 @@ def wgrad(G, X):
     return out
 
 
+def colsum(x):
+    """(R, C) fp32 / bf16 / fp16 with unit column stride -> (C,) fp32 column sums (mc_colsum): fixed row
+    slices, folded in order -- deterministic, no cross-workgroup hand-off inside the launch (torch's
+    reduction of the same shape combines workgroups through a staging buffer and returned wrong sums
+    beside concurrent library GEMMs: DESIGN.md 4.9)."""
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    R, C = x.shape
+    out = torch.empty(C, device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    ws_b = lib.mc_colsum_workspace_bytes(R, C)
+    ws = _ws(ws_b, x.device)
+    _lib.check(lib.mc_colsum(R, C, _lib.dtype_code(x.dtype), x.data_ptr(), x.stride(0), out.data_ptr(), ws.data_ptr(),
+                             ws_b, _lib.stream_handle(x.device)), "mc_colsum")
+    return out
+
+
+class L2NormalizeFn(torch.autograd.Function):
+    """torch.nn.functional.normalize(x, dim=-1) for 2-D x (the towers' output features, reference
+    model.py:1011-1017): fp32 out; one wave per row each way (mc_l2norm_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        x2 = x if x.stride(-1) == 1 else x.contiguous()
+        R, C = x2.shape
+        y = torch.empty(R, C, device=x.device, dtype=torch.float32)
+        norm = torch.empty(R, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().mc_l2norm_fwd(R, C, _lib.dtype_code(x2.dtype), x2.data_ptr(), x2.stride(0), eps,
+                                             y.data_ptr(), C, norm.data_ptr(), _lib.stream_handle(x.device)),
+                   "mc_l2norm_fwd")
+        ctx.save_for_backward(x2, norm)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, norm = ctx.saved_tensors
+        g = g.float()
+        if g.stride(-1) != 1:
+            g = g.contiguous()
+        R, C = x2.shape
+        dx = torch.empty(R, C, device=x2.device, dtype=x2.dtype)
+        _lib.check(_lib.load().mc_l2norm_bwd(R, C, _lib.dtype_code(x2.dtype), x2.data_ptr(), x2.stride(0),
+                                             norm.data_ptr(), ctx.eps, g.data_ptr(), g.stride(0), dx.data_ptr(), C,
+                                             _lib.stream_handle(x2.device)), "mc_l2norm_bwd")
+        return dx, None
+
+
+def l2_normalize(x, eps=1e-12):
+    """F.normalize(x, dim=-1) on the GPU kernels for 2-D CUDA tensors (fp32 result); torch elsewhere."""
+    if x.is_cuda and x.dim() == 2 and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and x.shape[1] > 0:
+        return L2NormalizeFn.apply(x, eps)
+    return torch.nn.functional.normalize(x, dim=-1, eps=eps)
+
+
+class TokenEmbedFn(torch.autograd.Function):
+    """ViT token embedding: m = cat([cls, x], 1) + pos, cls / pos cast to x's dtype (reference
+    model.py:232-358 via open_clip / timm's _pos_embed).  Same forward values as the torch ops; the
+    backward's batch reductions (d pos = sum_b dm, d cls = sum_b dm[:, 0] = d pos[0]) run as one
+    deterministic mc_colsum in fp32 instead of two torch reductions."""
+
+    @staticmethod
+    def forward(ctx, cls, x, pos):
+        B, N, C = x.shape
+        m = torch.cat([cls.to(x.dtype).expand(B, -1, -1), x], dim=1) + pos.to(x.dtype)
+        ctx.meta = (cls.dtype, pos.dtype, N)
+        return m
+
+    @staticmethod
+    def backward(ctx, dm):
+        cls_dt, pos_dt, N = ctx.meta
+        B, _, C = dm.shape
+        dpos = colsum(dm.reshape(B, (N + 1) * C)).view(1, N + 1, C)
+        dcls = dpos[:, :1].clone()
+        return dcls.to(cls_dt), dm[:, 1:], dpos.to(pos_dt)
+
+
+def token_embed(cls, x, pos):
+    if x.is_cuda and cls.requires_grad and pos.requires_grad:
+        return TokenEmbedFn.apply(cls, x, pos)
+    return torch.cat([cls.to(x.dtype).expand(x.shape[0], -1, -1), x], dim=1) + pos.to(x.dtype)
+
+
+class AddPosFn(torch.autograd.Function):
+    """h + pos[:, :T] for (B, T, C) h and a (1, Tmax, C) position table (BERT's position embedding):
+    the table's gradient is a deterministic batch column sum (mc_colsum), rows >= T zero."""
+
+    @staticmethod
+    def forward(ctx, h, pos):
+        T = h.shape[1]
+        ctx.meta = (pos.shape, pos.dtype, h.dtype)
+        return h + pos[:, :T]
+
+    @staticmethod
+    def backward(ctx, g):
+        pshape, pdt, hdt = ctx.meta
+        B, T, C = g.shape
+        dpos = torch.zeros(pshape, device=g.device, dtype=pdt)
+        dpos[:, :T] = colsum(g.reshape(B, T * C)).view(1, T, C).to(pdt)
+        return g, dpos
+
+
+def add_pos(h, pos):
+    if h.is_cuda and pos.requires_grad:
+        return AddPosFn.apply(h, pos)
+    return h + pos[:, : h.shape[1]]
+
+
 def sum_rows(t):
     """(R, n) fp32 contiguous -> (n,) column sums in a fixed order: two mc_sum_slabs passes (R -> R/16
     -> 1) when R is a multiple of 16, so each pass has enough workgroups (one pass over R = 256 rows
@@ -996,6 +1104,8 @@ class LinearSK(torch.autograd.Function):
             pre = getattr(gy, COLSUM_ATTR, None)   # column sums taken by the producer of gy (LayerNorm bwd)
             if pre is not None and pre[1] == gy._version and pre[0].shape[0] == g2.shape[1]:
                 db = pre[0]
+            elif g2.is_cuda:
+                db = colsum(g2)
             else:
                 db = torch.sum(g2, 0, dtype=torch.float32)
         return dx, dw, db

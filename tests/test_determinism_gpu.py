@@ -1,0 +1,115 @@
+"""Run-to-run reproducibility of the training step.
+
+* One stream (ClipModel.concurrent_towers False): the C2 model (real widths, batch 32) trained for three
+  AdamW steps twice in one process ends with bitwise-equal parameters.
+* Two streams on ONE hardware queue (GPU_MAX_HW_QUEUES=1, set before HIP starts, so a subprocess): the
+  same, with the towers concurrent -- the configuration measured reproducible in every run
+  (profiles/r05/determinism/); with several hardware queues the Mamba tower's scan-backward gradients
+  still vary from run to run in some timings.
+* The reductions that replaced torch's in the towers' glue (mc_colsum, mc_l2norm) give the same bits
+  beside concurrent library GEMMs as on an idle device (torch's cross-workgroup batch sum did not:
+  ~0.1 % of its outputs were wrong, tools/sum_under_load.py)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent('''
+    import os, sys
+    sys.path.insert(0, os.path.join(sys.argv[1], "mamba-clip_amd"))
+    import torch
+    from types import SimpleNamespace
+    from mamba_clip_amd import train
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import build_clip
+    concurrent = sys.argv[2] == "1"
+    batch = int(sys.argv[3])
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = build_clip("vit_b16-mamba130m").to(dev)
+    model.concurrent_towers = concurrent
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    images, texts, _ = synthetic_batch(batch, 224, model.text.context_length, model.text.vocab_size,
+                                       device=dev, seed=1000)
+    args = SimpleNamespace(precision="amp_bf16", lr=5e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
+                           grad_clip_norm=None, accum_freq=1)
+    finals = []
+    for rep in range(2):
+        model.load_state_dict(init)
+        opt = train.create_optimizer(model, args)
+        for s in range(3):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(images, texts)
+                loss = ClipLoss()(**out)["contrastive_loss"]
+            loss.backward()
+            train.optimizer_step(model, opt, None, args)
+            del out, loss
+        torch.cuda.synchronize()
+        finals.append([p.detach().clone() for p in model.parameters()])
+    same = all(torch.equal(a, b) for a, b in zip(*finals))
+    moved = any(not torch.equal(a, init_p) for a, init_p in zip(finals[0], init.values()))
+    print("RESULT", int(same), int(moved), int(model._side_stream(images, texts) is not None))
+''')
+
+
+def _run(concurrent, batch, hw_queues=None):
+    env = dict(os.environ)
+    if hw_queues is not None:
+        env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
+    r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, "1" if concurrent else "0", str(batch)],
+                       capture_output=True, text=True, env=env, timeout=300)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")]
+    assert r.returncode == 0 and line, r.stderr[-2000:]
+    return [int(x) for x in line[0].split()[1:]]
+
+
+def test_one_stream_three_steps_bitwise_reproducible():
+    same, moved, two = _run(concurrent=False, batch=32)
+    assert moved and not two
+    assert same
+
+
+def test_two_streams_one_hw_queue_three_steps_bitwise_reproducible():
+    same, moved, two = _run(concurrent=True, batch=32, hw_queues=1)
+    assert moved and two, "the towers did not run on two streams"
+    assert same
+
+
+def test_glue_reductions_beside_concurrent_gemms():
+    from mamba_clip_amd import ops
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    m = torch.empty(256, 197 * 768, device=dev, dtype=torch.bfloat16)
+    f = torch.empty(256, 512, device=dev, dtype=torch.bfloat16)
+    gf = torch.empty(256, 512, device=dev)
+    a = torch.randn(50432, 768, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(3072, 768, device=dev, generator=g).to(torch.bfloat16)
+    side = torch.cuda.Stream()
+
+    def victims():
+        fx = f.detach().requires_grad_(True)
+        y = ops.l2_normalize(fx)
+        y.backward(gf)
+        return [ops.colsum(m), y.detach(), fx.grad]
+    for _ in range(20):
+        m.normal_(generator=g)
+        f.normal_(generator=g)
+        gf.normal_(generator=g)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                torch.nn.functional.linear(a, w)
+        busy = victims()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        idle = victims()
+        for x, y in zip(busy, idle):
+            assert torch.equal(x, y)

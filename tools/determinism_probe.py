@@ -45,6 +45,14 @@ def main():
                          "(step-1 grads, final params, losses) and their first differing grads in backward order")
     ap.add_argument("--self-ref", action="store_true",
                     help="with --summary: compare each variant's runs with an extra first run of that variant")
+    ap.add_argument("--isolate", default="",
+                    help="comma list of mc_* library calls to run alone on the device: a device synchronize before "
+                         "and after each such call (is that kernel a victim or an aggressor of the two-stream race?)")
+    ap.add_argument("--isolate-aten", default="",
+                    help="comma list of aten op name prefixes (sum, mm, bmm, addmm, ...) to run alone on the device")
+    ap.add_argument("--pre-sync", default="none", choices=["none", "other", "current", "device", "other_event", "clone_bias", "clone_D", "clone_A"],
+                    help="before each scan backward: host-wait for the other stream / this stream / the device, or "
+                         "make this stream wait (event) for the other stream's work so far")
     ap.add_argument("--fill-nan", action="store_true",
                     help="torch.use_deterministic_algorithms(warn_only) + fill_uninitialized_memory: every torch.empty "
                          "is NaN-filled, so a kernel reading memory it never wrote shows up")
@@ -63,6 +71,26 @@ def main():
 
     dev = torch.device("cuda", 0)
     load_gemm_tuning(model=args.model)
+    if args.isolate:
+        from mamba_clip_amd import _lib
+        iso = set(args.isolate.split(","))
+
+        class _Iso:
+            def __init__(self, lib):
+                self._lib = lib
+
+            def __getattr__(self, name):
+                fn = getattr(self._lib, name)
+                if name not in iso:
+                    return fn
+
+                def call(*a):
+                    torch.cuda.synchronize()
+                    rc = fn(*a)
+                    torch.cuda.synchronize()
+                    return rc
+                return call
+        _lib._lib = _Iso(_lib.load())
     targs = SimpleNamespace(precision="amp_bf16", lr=5e-4, wd=0.2, beta1=0.9, beta2=0.98, eps=1e-6,
                             grad_clip_norm=None, accum_freq=1)
     torch.manual_seed(0)
@@ -75,7 +103,61 @@ def main():
     names = [n for n, _ in model.named_parameters()]
     img_names = {n for n in names if n.startswith("visual.")}
 
+    iso_mode = None
+    if args.isolate_aten:
+        from torch.utils._python_dispatch import TorchDispatchMode
+        pref = tuple(args.isolate_aten.split(","))
+
+        class _IsoAten(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, a=(), kw=None):
+                name = func.__name__.split(".")[0]
+                if name in pref:
+                    torch.cuda.synchronize()
+                    out = func(*a, **(kw or {}))
+                    torch.cuda.synchronize()
+                    return out
+                return func(*a, **(kw or {}))
+        iso_mode = _IsoAten()
+
+    nn_stream = torch.cuda.Stream(device=dev)
+    if args.pre_sync != "none":
+        from mamba_clip_amd import selective_scan_interface as ssi
+        real_bwd = ssi.scan_bwd
+        default = torch.cuda.default_stream(dev)
+
+        def wrapped(*a, **k):
+            cur = torch.cuda.current_stream(dev)
+            other = model.side_stream_for(dev) if cur == default else default
+            if args.pre_sync == "other":
+                other.synchronize()
+            elif args.pre_sync == "current":
+                cur.synchronize()
+            elif args.pre_sync == "device":
+                torch.cuda.synchronize()
+            elif args.pre_sync == "other_event":
+                cur.wait_stream(other)
+            elif args.pre_sync.startswith("clone_"):   # scan_bwd(u, delta, A, B, C, D, z, delta_bias, ...)
+                a = list(a)
+                j = {"clone_bias": 7, "clone_D": 5, "clone_A": 2}[args.pre_sync]
+                a[j] = a[j].clone()
+            return real_bwd(*a, **k)
+        ssi.scan_bwd = wrapped
+
     def run(variant):
+        if variant.endswith("_nn"):   # the whole step on a non-default stream (not HIP's null stream)
+            cur = torch.cuda.current_stream()
+            nn_stream.wait_stream(cur)
+            with torch.cuda.stream(nn_stream):
+                rec = run_(variant[:-3])
+            cur.wait_stream(nn_stream)
+            torch.cuda.synchronize()
+            return rec
+        if iso_mode is not None:
+            with iso_mode:
+                return run_(variant)
+        return run_(variant)
+
+    def run_(variant):
         model.load_state_dict(init)
         model.zero_grad(set_to_none=True)
         model.concurrent_towers = not variant.startswith("seq")
@@ -83,12 +165,15 @@ def main():
         os.environ.pop("MAMBA_CLIP_AMD_FINE_STATES_MB", None)
         if variant.startswith("conc_text"):
             os.environ["MAMBA_CLIP_AMD_SIDE_TOWER"] = "text"
+        elif variant.startswith("conc_image"):
+            os.environ["MAMBA_CLIP_AMD_SIDE_TOWER"] = "image"
         if variant.endswith("_nofine"):
             os.environ["MAMBA_CLIP_AMD_FINE_STATES_MB"] = "0"
         for m in model.modules():
             if hasattr(m, "fused_attention"):
                 m.fused_attention = not variant.endswith("_noattn")
         ops.WGRAD_HIP = variant.endswith("_wgradhip")
+        torch.backends.cuda.preferred_blas_library("cublas" if variant.endswith("_rocblas") else "cublaslt")
         ops.WCAST_T = variant != "conc_nowt"
         ClipModel.shared_weight_casts = variant.endswith("_sharedcast")
         hip = train.HIP_ADAMW
@@ -122,6 +207,14 @@ def main():
         torch.cuda.synchronize()
         rec["loss"] = [float(x) for x in losses]
         rec["params"] = {n: p.detach().clone() for n, p in model.named_parameters()}
+
+        def fp(t):   # exact fingerprint of a tensor's bits
+            b = t.detach().contiguous().view(-1)
+            b = b.view(torch.int16).to(torch.int64) if b.element_size() == 2 else b.view(torch.int32).to(torch.int64)
+            w = torch.arange(1, b.numel() + 1, device=b.device, dtype=torch.int64) % 1000003
+            return int((b * w).sum())
+        rec["fp_grads"] = hash(tuple(fp(v) for v in rec["grads"].values()))
+        rec["fingerprint"] = hash((rec["fp_grads"], tuple(fp(v) for v in rec["params"].values())))
         del opt
         return rec
 
@@ -150,17 +243,25 @@ def main():
             if args.self_ref:
                 run(variant)            # warm-up: a variant switch rebuilds plans / registrations on its first run
                 ref = run(variant)
+            fps, fpg = [], []
             for r in range(args.repeats):
                 rec = run(variant)
+                fps.append(rec["fingerprint"])
+                fpg.append(rec["fp_grads"])
                 bad = [n for n in order if not torch.equal(ref["grads"][n], rec["grads"][n])]
                 pbad = sum(1 for n in names if not torch.equal(ref["params"][n], rec["params"][n]))
                 if bad or pbad or rec["loss"] != ref["loss"]:
-                    print(json.dumps({"variant": variant, "repeat": r, "fine_live_mb": rec["fine_live_mb"],
-                                      "ref_fine_live_mb": ref["fine_live_mb"], "first_bad": bad[:2]}), flush=True)
+                    pnames = [n for n in order if not torch.equal(ref["params"][n], rec["params"][n])]
+                    print(json.dumps({"variant": variant, "repeat": r, "first_bad": bad[:2],
+                                      "loss_equal_per_step": [a == b for a, b in zip(ref["loss"], rec["loss"])],
+                                      "n_params_differ": len(pnames), "params_differ_first": pnames[:4],
+                                      "params_differ_img": sum(1 for n in pnames if n in img_names)}), flush=True)
                     bad_runs += 1
                     key = ",".join(bad[:2]) if bad else "params-only"
                     firsts[key] = firsts.get(key, 0) + 1
             summ[variant] = {"runs": args.repeats, "runs_differ": bad_runs, "first_bad": firsts,
+                             "distinct_outcomes": len(set(fps)), "distinct_step1_grads": len(set(fpg)),
+                             "ref_step1_grads_seen_again": fpg.count(ref["fp_grads"]),
                              "s": round(time.time() - t0, 1)}
             print(json.dumps({"variant": variant, **summ[variant]}), flush=True)
         if args.out:

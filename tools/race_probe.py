@@ -81,9 +81,32 @@ def main():
     def bwd(*a, **k):
         if args.light:
             ins = tuple(csum(x) for x in a)
-            out = real_bwd(*a, **k)
-            calls.append(("bwd", ins, (out[2].clone(), out[5].clone() if out[5] is not None else None,
-                                       out[7].clone() if out[7] is not None else None)))
+            wss = []
+            real_empty = torch.empty
+
+            def empty(*sz, **kw):       # catch the workspace (the one uint8 allocation of scan_bwd)
+                t = real_empty(*sz, **kw)
+                if kw.get("dtype") is torch.uint8:
+                    wss.append(t)
+                return t
+            torch.empty = empty
+            try:
+                out = real_bwd(*a, **k)
+            finally:
+                torch.empty = real_empty
+            # pair-path workspace (scan_bwd.hip bwd_ws_layout): [bq][slab_bc][slab_a][slab_d][slab_bias], 256-B aligned
+            u_, delta_ = a[0], a[1]
+            bsz, dim, L = delta_.shape
+            al = lambda x: (x + 255) // 256 * 256
+            nblk = (dim + 63) // 64
+            o_bc = al(bsz * L * 8 * 16)
+            o_a = o_bc + al(bsz * nblk * 16 * 2 * L * 4)
+            o_d = o_a + al(bsz * dim * 16 * 4)
+            o_b = o_d + al(bsz * dim * 4)
+            ws = wss[0] if wss else None
+            slabs = (ws[o_d:o_d + bsz * dim * 4].clone(), ws[o_b:o_b + bsz * dim * 4].clone()) if ws is not None else ()
+            outs = tuple(csum(x) for x in out) + slabs
+            calls.append(("bwd", ins, outs + (out[2].clone(), out[7].clone() if out[7] is not None else None)))
             return out
         ins = snap(a)          # the inputs as the kernel will read them (same stream: ordered)
         out = real_bwd(*a, **k)

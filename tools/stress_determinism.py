@@ -63,6 +63,7 @@ def main():
     x_s = torch.randn(8, (Bsz * L) // 8, 1536, device=dev, generator=g).to(bf)
     vit_x = torch.randn(50432, 768, device=dev, generator=g).to(bf)
     vit_w = torch.randn(3072, 768, device=dev, generator=g).to(bf)
+    vit_m = torch.randn(256, 197, 768, device=dev, generator=g).to(bf)
 
     def run(op):
         if op == "scan_bwd":
@@ -89,6 +90,12 @@ def main():
             return torch.mm(w_in, h_cm)
         if op == "gemm_out_dgrad":    # out_proj's input gradient into the channel-major layout
             return torch.mm(w_out.t(), g_out.t()).t()
+        if op == "sum0":             # the ViT's pos_embed gradient: a bf16 (B, 197, 768) summed over the batch
+            return vit_m.sum(0, keepdim=True)
+        if op == "sum_cls":          # cls_token: the batch sum of one row
+            return vit_m[:, :1].sum(0, keepdim=True)
+        if op == "colsum_f32":       # a bias gradient: fp32 column sums of (B*L, C)
+            return torch.sum(vit_x, 0, dtype=torch.float32)
         if op == "bmm_f32":           # the split-K weight-gradient slabs (ops.wgrad library path)
             return torch.bmm(g_s, x_s, out_dtype=torch.float32)
         raise ValueError(op)
@@ -114,6 +121,12 @@ def main():
         elif kind == "scan":
             for _ in range(4):
                 ssi.scan_bwd(u2, delta, A, Bm, Cm, Dv, z2, bias, True, d2, st_fine)
+        elif kind == "scan_nofine":
+            for _ in range(4):
+                ssi.scan_bwd(u2, delta, A, Bm, Cm, Dv, z2, bias, True, d2, st_def)
+        elif kind == "scan_fwd":
+            for _ in range(4):
+                ssi.scan_fwd(u2, delta, A, Bm, Cm, Dv, z2, bias, True, True, False)
 
     def eq(a, b):
         if isinstance(a, torch.Tensor):
