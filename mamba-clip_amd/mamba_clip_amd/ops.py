@@ -708,8 +708,10 @@ def wgrad_hip(G, X, splits=0):
     return out
 
 
-# A/B toggle: the towers' weight gradients on mc_gemm_wgrad (1) or the library's split-K slabs (0)
-WGRAD_HIP = os.environ.get("MAMBA_CLIP_AMD_WGRAD_HIP", "0") != "0"
+# The towers' long-K weight gradients on mc_gemm_wgrad (csrc/gemm_wgrad.hip, on by default since round 5:
+# 1.0-1.1 PFLOP/s vs the library split-K slabs' 0.75-0.91 at the ViT / Mamba shapes, same-box step
+# C2 69.96 -> 68.5 ms, C3 25.4 -> 25.0 ms, profiles/r05/wgrad/); 0 = the library slabs (A/B)
+WGRAD_HIP = os.environ.get("MAMBA_CLIP_AMD_WGRAD_HIP", "1") != "0"
 
 
 def wgrad(G, X):

@@ -85,6 +85,7 @@ def test_wgrad_c2_shape_and_linear_backward():
     w = torch.randn(3072, 768, device=DEV, requires_grad=True)
     gy = torch.randn(64, 197, 3072, device=DEV, dtype=torch.bfloat16)
     grads = {}
+    prev = ops.WGRAD_HIP
     for on in (False, True):
         ops.WGRAD_HIP = on
         try:
@@ -92,7 +93,7 @@ def test_wgrad_c2_shape_and_linear_backward():
             ops.linear_sk(x, w).backward(gy)
             grads[on] = w.grad.clone()
         finally:
-            ops.WGRAD_HIP = False
+            ops.WGRAD_HIP = prev
     ref = gy.reshape(-1, 3072).double().t() @ x.detach().reshape(-1, 768).double()
     for on in (False, True):
         assert float((grads[on].double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) * 50
