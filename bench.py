@@ -125,10 +125,13 @@ def scan_roofline(iters, warmup=10):
     torch.cuda.empty_cache()
     copy_gbs = _copy_bandwidth(dev)
     traffic, traffic_src = _pmc_traffic()
+    valu_frac, valu_src = _pmc_valu()
     return {"kernel": "selective_scan_fwd (scan_fwd_pair_kernel, B/C rows read in-kernel) @ C4 B64 D3072 L4096 N16 bf16 z softplus",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": traffic_src, "traffic_measured_in_this_run": False,
+            # the kernel is VALU-issue bound, not HBM bound: VALU busy cycles / SIMD cycles (PMC)
+            "valu_frac": valu_frac, "valu_frac_source": valu_src,
             "ms_per_call": round(ms, 4), "algorithmic_bytes": nbytes,
             # also report the achievable copy bandwidth measured on this box
             "copy_gbs_measured": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 4)}
@@ -224,6 +227,18 @@ def _pmc_traffic():
         return None, None
     d = json.load(open(files[-1]))
     return (int(d["hbm_bytes"]) if d.get("hbm_bytes") else None), os.path.relpath(files[-1], ROOT)
+
+
+def _pmc_valu():
+    """VALU issue fraction of the same kernel at the same config: 4 * SQ_ACTIVE_INST_VALU
+    (quad-cycles) / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 XCDs), from the committed rocprofv3 pass
+    (tools/pmc_valu.sh; counters and derivation in the JSON)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "scan_fwd_c4_valu.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("valu_frac"), os.path.relpath(files[-1], ROOT)
 
 
 def _cpu_threads(args):
