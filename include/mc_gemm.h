@@ -2,6 +2,8 @@
  * mc_gemm.h -- C ABI of the MI355X weight-gradient GEMM (libmamba_clip_amd.so, csrc/gemm_wgrad.hip).
  *
  *   mc_gemm_wgrad   C (M x N, fp32) = sum over T of A(t, m) B(t, n), bf16 / f16 operands
+ *   mc_linear       Y (rows x cols, 16-bit) = X W^T with a fused epilogue (bias, bias + GELU, GELU'),
+ *                   the towers' Linear forward / input-gradient GEMMs on the same 256 x 256 kernel
  *
  * It replaces the library GEMM behind every tower Linear's weight gradient, dW = G^T X
  * (reference: the towers' Linear / MLP layers behind encode_image / encode_text,
@@ -50,6 +52,49 @@ typedef struct mc_wgrad_params {
 
 size_t mc_gemm_wgrad_workspace_bytes(const mc_wgrad_params* p);
 int mc_gemm_wgrad(const mc_wgrad_params* p, void* stream);
+
+/*
+ * mc_linear: Y[t][f] = sum_k X[t][k] W[f][k] (+ epilogue), fp32 accumulation, Y rounded once to the
+ * operand dtype.  The forward of a tower Linear (X = input, W = weight) and its input gradient
+ * (X = output gradient, W = the TRANSPOSED weight copy, (in, out)) -- reference: the towers' Linear /
+ * MLP layers behind encode_image / encode_text, model.py:1011-1017 (timm Mlp: fc1 -> nn.GELU() exact
+ * erf -> fc2).  Epilogues:
+ *   MC_LINEAR_EPI_NONE       Y = XW^T
+ *   MC_LINEAR_EPI_BIAS       Y = XW^T + bias
+ *   MC_LINEAR_EPI_BIAS_GELU  Y = h = XW^T + bias (the pre-activation, kept for the backward) and
+ *                            Y2 = gelu(h) = h * Phi(h), exact erf, of the ROUNDED h (as torch's
+ *                            F.gelu of the stored h) -- fc1 + GELU in one pass
+ *   MC_LINEAR_EPI_GELU_GRAD  Y = round(XW^T) * gelu'(H) -- fc2's input gradient times GELU's
+ *                            derivative at fc1's saved pre-activation H, rounded as torch's
+ *                            gelu_backward of the stored fc2 input gradient; with `colsum`, also
+ *                            the fp32 column sums of Y as stored (fc1's bias gradient), per
+ *                            256-token tile into the workspace and folded in a fixed order
+ * Requirements: K % 64 == 0, cols % 8 == 0, 16-B aligned bases, leading dims % 8 == 0, unit stride
+ * along K (X, W) and along the features (Y, Y2, H).  Deterministic: one workgroup per output tile.
+ */
+#define MC_LINEAR_EPI_NONE 0
+#define MC_LINEAR_EPI_BIAS 1
+#define MC_LINEAR_EPI_BIAS_GELU 2
+#define MC_LINEAR_EPI_GELU_GRAD 3
+
+typedef struct mc_linear_params {
+  int32_t rows, cols, K;         /* tokens, output features, reduction */
+  int32_t dtype;                 /* MC_DTYPE_BF16 / MC_DTYPE_F16 (X, W, Y, Y2, H) */
+  int32_t epilogue;              /* MC_LINEAR_EPI_* */
+  int32_t reserved;
+  const void* X; int64_t ldx;    /* (rows, K) */
+  const void* W; int64_t ldw;    /* (cols, K) */
+  void* Y; int64_t ldy;          /* (rows, cols) */
+  void* Y2; int64_t ldy2;        /* BIAS_GELU: (rows, cols) gelu(h) */
+  const void* bias;              /* BIAS / BIAS_GELU: (cols,) in the operand dtype, 8-B aligned */
+  const void* H; int64_t ldh;    /* GELU_GRAD: (rows, cols) pre-activation */
+  float* colsum;                 /* GELU_GRAD, optional: (cols,) column sums of Y */
+  void* workspace;               /* >= mc_linear_workspace_bytes(p) when colsum is set, 16-B aligned */
+  size_t workspace_bytes;
+} mc_linear_params;
+
+size_t mc_linear_workspace_bytes(const mc_linear_params* p);
+int mc_linear(const mc_linear_params* p, void* stream);
 
 #ifdef __cplusplus
 }

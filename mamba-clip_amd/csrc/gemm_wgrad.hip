@@ -55,7 +55,21 @@ struct Args {
   int64_t lda, ldb;          // elements
   float* C; int64_t ldc;     // output (splits == 1) or slab base (slab s at C + s * slab_stride)
   int64_t slab_stride;
+  // 16-bit epilogues (kEpi != kEpiSlab, mc_linear): the tile is stored TRANSPOSED, Y[n][m] -- n the
+  // token (Y's row), m the feature (Y's column)
+  void* Y; int64_t ldy;
+  void* Y2; int64_t ldy2;    // kEpiBiasGelu: gelu(h)
+  const void* bias;          // kEpiBias / kEpiBiasGelu: per feature m, operand dtype
+  const void* H; int64_t ldh;   // kEpiGeluGrad: pre-activation at Y's positions
+  float* colpart;            // kEpiGeluGrad: column sums of Y per token tile, [tiles_n][M] (or null)
 };
+
+// epilogues of wgrad4p_kernel
+constexpr int kEpiSlab = 0;       // fp32 C (or split-K slab), row m / column n
+constexpr int kEpiStore = 1;      // Y = C^T, 16-bit
+constexpr int kEpiBias = 2;       // Y = C^T + bias
+constexpr int kEpiBiasGelu = 3;   // Y = h = C^T + bias, Y2 = gelu(h)
+constexpr int kEpiGeluGrad = 4;   // Y = round(C^T) * gelu'(H), column sums of Y
 
 // One global_load_lds_dwordx4: 16 B per lane from gsrc to LDS byte address m0v + 16 * lane (m0v
 // wave-uniform).  asm, so hipcc's waitcnt pass does not drain it at the next LDS read; the loop
@@ -281,7 +295,11 @@ __device__ __forceinline__ void half_sources(const char* base, int64_t ld, int d
 // (lgkmcnt(0)) BEFORE its first barrier: the half-tile restaged one phase later is only written after
 // that barrier, which both rows have passed with their reads of it done (cdna_hip_programming.md
 // section 5: "one barrier MORE when two wave groups run staggered").
-template <typename T, bool kAFM, bool kBFM, bool kStagger>
+template <typename T, int kEpi>
+__device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4 (&acc)[2][2][4][2], int m0, int n0,
+                                           int tn, int wr, int wc, int fg, int fi, int tid);
+
+template <typename T, bool kAFM, bool kBFM, bool kStagger, int kEpi = kEpiSlab>
 __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 4 * kHalf];   // [stage][A h0, A h1, B h0, B h1]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -447,6 +465,10 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
   }
   if (kStagger && wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both rows
 
+  if constexpr (kEpi != kEpiSlab) {
+    epilogue16<T, kEpi>(g, lds, acc, m0, n0, tn, wr, wc, fg, fi, tid);
+    return;
+  }
   // ---- epilogue: quadrant (qm, qn), tile (mi, ni): rows wr*128 + qm*64 + mi*16 + 4 (l >> 4) + r,
   // column wc*64 + qn*32 + ni*16 + (l & 15)
   float* C = g.C + (int64_t)split * g.slab_stride;
@@ -465,6 +487,116 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
             if (row < g.M && col < g.N) C[(int64_t)row * g.ldc + col] = acc[qm][qn][mi][ni][r];
           }
         }
+}
+
+// 16-bit epilogue through LDS.  Every wave is past its last fragment read (the K loop's closing
+// barrier), so the stage memory becomes the image of the transposed output tile: 256 token rows of
+// 512 B (256 features), 16-B chunk c of row n at slot c ^ (n & 31).  A lane holds 4 consecutive
+// features of one token per accumulator (rows 4 (l >> 4) + r of the MFMA tile): one 8-B LDS write
+// each, the bias added before the rounding.  Then the workgroup walks the image row by row -- a
+// wave moves two whole 512-B rows -- and writes Y (and Y2 / reads H) with full-line 16-B accesses;
+// GELU / GELU' are evaluated there, on coalesced vectors.  The column sums (kEpiGeluGrad) meet in
+// LDS in a fixed order: one fp32 partial per (token tile, feature), folded by the caller.
+template <typename T, int kEpi>
+__device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4 (&acc)[2][2][4][2], int m0, int n0,
+                                           int tn, int wr, int wc, int fg, int fi, int tid) {
+  const int c = tid & 31, sub = tid >> 5;   // read-back: chunk of 8 features, row within a group of 16
+  const int f = m0 + c * 8;
+  const bool fok = f < g.M;
+  // kEpiGeluGrad: this thread's 16 vectors of H, requested before the staging pass so their latency
+  // hides behind it (the accumulators' registers are still live; H takes 64 more)
+  uint4 hq[16];
+  if constexpr (kEpi == kEpiGeluGrad) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int t = min(n0 + p * 16 + sub, g.N - 1);
+      hq[p] = fok ? ld16(reinterpret_cast<const T*>(g.H) + (int64_t)t * g.ldh + f) : make_uint4(0, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int m = wr * 128 + qm * 64 + mi * 16 + 4 * fg;   // 4 consecutive features
+      f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (kEpi == kEpiBias || kEpi == kEpiBiasGelu) {
+        if (m0 + m < g.M) {
+          const uint2 bq = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(g.bias) + m0 + m);
+          const uint4 b4 = make_uint4(bq.x, bq.y, 0u, 0u);
+          b = f32x4{elem_f<T>(b4, 0), elem_f<T>(b4, 1), elem_f<T>(b4, 2), elem_f<T>(b4, 3)};
+        }
+      }
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int n = wc * 64 + qn * 32 + ni * 16 + fi;     // token
+          const f32x4 v = acc[qm][qn][mi][ni] + b;
+          const uint2 pk = make_uint2(cvt_pk2<T>(v[0], v[1]), cvt_pk2<T>(v[2], v[3]));
+          *reinterpret_cast<uint2*>(lds + n * 512 + ((((m >> 3) ^ (n & 31))) << 4) + (m & 7) * 2) = pk;
+        }
+    }
+  __syncthreads();
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  if constexpr (kEpi == kEpiGeluGrad) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int n = p * 16 + sub;
+      const int t = n0 + n;
+      const uint4 q = *reinterpret_cast<const uint4*>(lds + n * 512 + ((c ^ (n & 31)) << 4));
+      if (!fok || t >= g.N) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float phi, pdf;
+        const float x = elem_f<T>(hq[p], e);
+        phi_pdf_f(x, phi, pdf);
+        o[e] = elem_f<T>(q, e) * fmaf(x, pdf, phi);
+      }
+      const uint4 oq = pack_f<T>(o);
+      st16(reinterpret_cast<T*>(g.Y) + (int64_t)t * g.ldy + f, oq);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += elem_f<T>(oq, e);
+    }
+  } else {
+#pragma unroll 1
+    for (int p0 = 0; p0 < 16; p0 += 4) {
+      uint4 q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = (p0 + j) * 16 + sub;
+        q[j] = *reinterpret_cast<const uint4*>(lds + n * 512 + ((c ^ (n & 31)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = n0 + (p0 + j) * 16 + sub;
+        if (!fok || t >= g.N) continue;
+        st16(reinterpret_cast<T*>(g.Y) + (int64_t)t * g.ldy + f, q[j]);
+        if constexpr (kEpi == kEpiBiasGelu) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = gelu_f(elem_f<T>(q[j], e));   // library erff, torch's F.gelu form
+          st16(reinterpret_cast<T*>(g.Y2) + (int64_t)t * g.ldy2 + f, pack_f<T>(o));
+        }
+      }
+    }
+  }
+  if constexpr (kEpi == kEpiGeluGrad) {
+    if (g.colpart == nullptr) return;
+    __syncthreads();                                   // the image is read: reuse it for the sums
+    float* red = reinterpret_cast<float*>(lds);        // [16 rows of the group][256 features]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[sub * 256 + c * 8 + e] = cs[e];
+    __syncthreads();
+    if (tid < 256 && m0 + tid < g.M) {
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += red[r * 256 + tid];
+      g.colpart[(int64_t)tn * g.M + m0 + tid] = s;
+    }
+  }
 }
 
 // MC_WGRAD_PIPE: 5 = four-phase pipeline with staggered wave rows (default), 4 = four-phase, rows in
@@ -568,5 +700,79 @@ extern "C" int mc_gemm_wgrad(const mc_wgrad_params* p, void* stream) {
   hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_wgrad: launch failed: %s", hipGetErrorString(e));
   if (splits > 1) return mc_sum_slabs(splits, (int64_t)p->M * p->N, a.C, a.slab_stride, p->C, stream);
+  return MC_OK;
+}
+
+// ------------------------------------------------------------------ mc_linear
+// Y = X W^T on wgrad4p_kernel with both operands feature-major in its terms (A = W: row m = output
+// feature, B = X: row n = token, unit stride along K) and a 16-bit epilogue; one workgroup per
+// 256 x 256 output tile (K <= a few thousand: no split).
+template <typename T>
+static void launch_linear(const Args& a, int epi, hipStream_t s) {
+  const dim3 grid(a.tiles_m * a.tiles_n), block(kThreads);
+  switch (epi) {
+    case MC_LINEAR_EPI_NONE: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiStore>), grid, block, 0, s, a); break;
+    case MC_LINEAR_EPI_BIAS: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiBias>), grid, block, 0, s, a); break;
+    case MC_LINEAR_EPI_BIAS_GELU:
+      hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiBiasGelu>), grid, block, 0, s, a);
+      break;
+    default: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiGeluGrad>), grid, block, 0, s, a); break;
+  }
+}
+
+static int linear_check(const mc_linear_params* p) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_linear: null params");
+  MC_CHECK(p->rows >= 0 && p->cols > 0 && p->K > 0 && p->cols % 8 == 0 && p->K % kBK == 0, MC_ERR_SHAPE,
+           "mc_linear: bad shape rows %d cols %d (%% 8) K %d (%% %d)", p->rows, p->cols, p->K, kBK);
+  MC_CHECK(p->dtype == MC_DTYPE_BF16 || p->dtype == MC_DTYPE_F16, MC_ERR_DTYPE, "mc_linear: operands must be bf16 or f16");
+  MC_CHECK(p->epilogue >= MC_LINEAR_EPI_NONE && p->epilogue <= MC_LINEAR_EPI_GELU_GRAD, MC_ERR_INVALID,
+           "mc_linear: bad epilogue %d", p->epilogue);
+  auto ok = [](const void* t, int64_t ld, int64_t width) { return t && aligned16(t) && ld % 8 == 0 && ld >= width; };
+  MC_CHECK(ok(p->X, p->ldx, p->K) && ok(p->W, p->ldw, p->K) && ok(p->Y, p->ldy, p->cols), MC_ERR_SHAPE,
+           "mc_linear: X, W, Y need 16-B aligned bases and leading dims %% 8 == 0 covering the row");
+  MC_CHECK((int64_t)p->rows * std::max(p->ldx, p->ldy) < ((int64_t)1 << 40), MC_ERR_SHAPE, "mc_linear: operand too large");
+  if (p->epilogue == MC_LINEAR_EPI_BIAS || p->epilogue == MC_LINEAR_EPI_BIAS_GELU)
+    MC_CHECK(p->bias && (reinterpret_cast<uintptr_t>(p->bias) & 7) == 0, MC_ERR_INVALID,
+             "mc_linear: the bias epilogues need an 8-B aligned bias (operand dtype)");
+  if (p->epilogue == MC_LINEAR_EPI_BIAS_GELU)
+    MC_CHECK(ok(p->Y2, p->ldy2, p->cols), MC_ERR_SHAPE, "mc_linear: BIAS_GELU needs Y2 (16-B aligned, ld %% 8 == 0)");
+  if (p->epilogue == MC_LINEAR_EPI_GELU_GRAD)
+    MC_CHECK(ok(p->H, p->ldh, p->cols), MC_ERR_SHAPE, "mc_linear: GELU_GRAD needs H (16-B aligned, ld %% 8 == 0)");
+  return MC_OK;
+}
+
+extern "C" size_t mc_linear_workspace_bytes(const mc_linear_params* p) {
+  if (linear_check(p) != MC_OK) return 0;
+  if (p->epilogue != MC_LINEAR_EPI_GELU_GRAD || p->colsum == nullptr) return 0;
+  return (size_t)((p->rows + kBN - 1) / kBN) * p->cols * 4;
+}
+
+extern "C" int mc_linear(const mc_linear_params* p, void* stream) {
+  int rc = linear_check(p);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const bool sums = p->epilogue == MC_LINEAR_EPI_GELU_GRAD && p->colsum != nullptr;
+  const int tiles_n = (p->rows + kBN - 1) / kBN;
+  if (sums) {
+    const size_t need = (size_t)tiles_n * p->cols * 4;
+    MC_CHECK(need == 0 || (p->workspace && p->workspace_bytes >= need && aligned16(p->workspace)), MC_ERR_WORKSPACE,
+             "mc_linear: workspace must be >= %zu bytes, 16-B aligned (got %zu)", need, p->workspace_bytes);
+  }
+  if (p->rows == 0) {
+    if (sums) (void)hipMemsetAsync(p->colsum, 0, (size_t)p->cols * 4, s);
+    return MC_OK;
+  }
+  Args a{};
+  a.M = p->cols; a.N = p->rows; a.T = p->K; a.splits = 1;
+  a.tiles_m = (p->cols + kBM - 1) / kBM; a.tiles_n = tiles_n; a.nk = p->K / kBK;
+  a.A = reinterpret_cast<const char*>(p->W); a.lda = p->ldw;
+  a.B = reinterpret_cast<const char*>(p->X); a.ldb = p->ldx;
+  a.Y = p->Y; a.ldy = p->ldy; a.Y2 = p->Y2; a.ldy2 = p->ldy2; a.bias = p->bias;
+  a.H = p->H; a.ldh = p->ldh; a.colpart = sums ? reinterpret_cast<float*>(p->workspace) : nullptr;
+  if (p->dtype == MC_DTYPE_BF16) launch_linear<bf16_t>(a, p->epilogue, s);
+  else launch_linear<f16_t>(a, p->epilogue, s);
+  hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_linear: launch failed: %s", hipGetErrorString(e));
+  if (sums) return mc_sum_slabs(tiles_n, p->cols, a.colpart, p->cols, p->colsum, stream);
   return MC_OK;
 }

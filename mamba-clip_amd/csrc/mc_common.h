@@ -220,6 +220,39 @@ __device__ __forceinline__ float sigmoid_f(float x) { return fast_rcp(1.f + fast
 
 __device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
 
+// GELU, exact erf form (torch F.gelu approximate='none': x * 0.5 * (1 + erf(x / sqrt2))) and its derivative
+__device__ __forceinline__ float gelu_f(float x) { return x * 0.5f * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {   // d/dx [x * Phi(x)]
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return fmaf(x, pdf, cdf);
+}
+// Phi(x) and pdf(x) = exp(-x^2/2)/sqrt(2 pi) from two v_exp_f32 and one v_rcp_f32 (the GEMM epilogues'
+// GELU / GELU', where the library erff's instruction count is not hidden behind memory): for
+// z = |x|/sqrt2, erfc(z) = t exp(-z^2 + P(t)), t = 1/(1 + z/2), P the degree-9 Chebyshev fit of
+// Numerical Recipes' erfcc (fractional error < 1.2e-7 for every z >= 0, so also in Phi's far tail);
+// exp(-z^2) is pdf's own exponential.
+__device__ __forceinline__ void phi_pdf_f(float x, float& phi, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);   // exp(-x^2/2)
+  const float erf_abs = 1.f - t * e * __builtin_amdgcn_exp2f(p * 1.4426950408889634f);   // erf(z), fp32
+  // torch's form 0.5 (1 + erf(x / sqrt2)), rounding included: for x << 0 the sum cancels exactly as
+  // F.gelu's does (e.g. gelu(-6) = -0 there), so the results match torch's, not the exact Phi
+  phi = 0.5f * (1.f + (x < 0.f ? -erf_abs : erf_abs));
+  pdf = 0.39894228040143268f * e;
+}
+
 // ---------------------------------------------------------------- host error plumbing
 void set_error(const char* fmt, ...);
 const char* last_error();

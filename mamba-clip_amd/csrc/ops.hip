@@ -800,11 +800,6 @@ __global__ __launch_bounds__(256) void im2col_kernel(int batch, int C, int H, in
 // to the activation dtype), like the unfused reduction.
 constexpr int kGradSlices = 512;
 
-__device__ __forceinline__ float gelu_grad_f(float x) {   // d/dx [x * Phi(x)], exact erf form (torch 'none')
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return fmaf(x, pdf, cdf);
-}
 
 template <typename T>
 __global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(int rows, int cols, const T* __restrict__ h, int64_t ldh,

@@ -213,6 +213,19 @@ class WgradParams(ctypes.Structure):
     ]
 
 
+MC_LINEAR_EPI_NONE, MC_LINEAR_EPI_BIAS, MC_LINEAR_EPI_BIAS_GELU, MC_LINEAR_EPI_GELU_GRAD = 0, 1, 2, 3
+
+
+class LinearParams(ctypes.Structure):
+    """Mirror of ``mc_linear_params`` (include/mc_gemm.h)."""
+    _fields_ = [
+        ("rows", c_i32), ("cols", c_i32), ("K", c_i32), ("dtype", c_i32), ("epilogue", c_i32), ("reserved", c_i32),
+        ("X", c_vp), ("ldx", c_i64), ("W", c_vp), ("ldw", c_i64), ("Y", c_vp), ("ldy", c_i64),
+        ("Y2", c_vp), ("ldy2", c_i64), ("bias", c_vp), ("H", c_vp), ("ldh", c_i64), ("colsum", c_vp),
+        ("workspace", c_vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 class PatchInputParams(ctypes.Structure):
     """Mirror of ``mc_patch_input_params`` (include/mc_ops.h)."""
     _fields_ = [
@@ -232,6 +245,8 @@ SYMBOLS = {
     "mc_scan_fwd_kernel": (c_i32, [ctypes.POINTER(ScanFwdParams)]),
     "mc_gemm_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradParams)]),
     "mc_gemm_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradParams), c_vp]),
+    "mc_linear_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(LinearParams)]),
+    "mc_linear": (ctypes.c_int, [ctypes.POINTER(LinearParams), c_vp]),
     "mc_scan_bwd_kernel": (c_i32, [ctypes.POINTER(ScanBwdParams)]),
     "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),

@@ -33,7 +33,7 @@ import torch.utils.checkpoint
 
 from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_pos, add_rmsnorm, attn_supported,
-                  causal_conv1d, fc1_gelu, l2_normalize, linear_sk, mixer_proj, mixer_proj_ok, neg_exp_many,
+                  causal_conv1d, l2_normalize, linear_sk, mixer_proj, mixer_proj_ok, mlp, neg_exp_many,
                   packed_attention, patch_im2col, qkv_proj, split_rows, split_rows_n, ss2d_conv_stack,
                   ss2d_merge_ln_gate, token_embed, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
@@ -316,7 +316,7 @@ class ViTBlock(nn.Module):
         y, h = add_layernorm(m, h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         a = self.attn(y)
         y, h = add_layernorm(a, h, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        return linear_sk(fc1_gelu(y, self.fc1.weight, self.fc1.bias), self.fc2.weight, self.fc2.bias), h
+        return mlp(y, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias), h
 
 
 class VisionTransformer(nn.Module):

@@ -1257,6 +1257,161 @@ def _hip_rows(t, V, who):
     return t if _aligned_rows(t, V) else t.clone(memory_format=torch.contiguous_format)
 
 
+# ---------------------------------------------------------------------------- towers' Linears on mc_linear
+# The forward / input-gradient GEMMs of the ViT Linears on the hand-written 256 x 256 kernel
+# (csrc/gemm_wgrad.hip, mc_linear) with the epilogues the library cannot fuse: bias + exact-erf GELU
+# for fc1 (one pass writes h and gelu(h)) and GELU' for fc2's input gradient (one pass writes
+# gh = ga * gelu'(h) and fc1's bias gradient).
+
+
+def linear_hip_ok(x2, w):
+    """x2 (rows, K) and w (cols, K) qualify for mc_linear: 16-bit, same dtype, unit stride along K,
+    K % 64, cols % 8, 16-B aligned rows."""
+    return (x2.is_cuda and x2.dim() == 2 and w.dim() == 2 and x2.dtype == w.dtype
+            and x2.dtype in (torch.bfloat16, torch.float16) and x2.shape[1] == w.shape[1]
+            and x2.shape[1] % 64 == 0 and x2.shape[1] > 0 and w.shape[0] % 8 == 0
+            and x2.stride(1) == 1 and w.stride(1) == 1 and x2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+def linear_hip(x2, w, bias=None, epilogue=None, h=None, want_colsum=False):
+    """x2 @ w^T on mc_linear with a fused epilogue (include/mc_gemm.h):
+    NONE / BIAS -> y; BIAS_GELU -> (h, gelu(h)); GELU_GRAD (h = the pre-activation) -> (gh, colsum or None).
+    The caller checks linear_hip_ok; a launch error raises (no library fallback inside)."""
+    if epilogue is None:
+        epilogue = _lib.MC_LINEAR_EPI_BIAS if bias is not None else _lib.MC_LINEAR_EPI_NONE
+    rows, K = x2.shape
+    cols = w.shape[0]
+    y = torch.empty(rows, cols, device=x2.device, dtype=x2.dtype)
+    p = _lib.LinearParams()
+    p.rows, p.cols, p.K, p.dtype, p.epilogue = rows, cols, K, _lib.dtype_code(x2.dtype), epilogue
+    p.X, p.ldx, p.W, p.ldw, p.Y, p.ldy = x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), cols
+    y2 = colsum_out = None
+    if bias is not None:
+        if bias.dtype != x2.dtype or bias.stride(0) != 1 or bias.data_ptr() % 8:
+            bias = bias.to(x2.dtype).contiguous()
+        p.bias = bias.data_ptr()
+    if epilogue == _lib.MC_LINEAR_EPI_BIAS_GELU:
+        y2 = torch.empty_like(y)
+        p.Y2, p.ldy2 = y2.data_ptr(), cols
+    ws = None
+    if epilogue == _lib.MC_LINEAR_EPI_GELU_GRAD:
+        h = _hip_rows(h, 8, "linear_hip GELU_GRAD")
+        p.H, p.ldh = h.data_ptr(), h.stride(0)
+        if want_colsum:
+            colsum_out = torch.empty(cols, device=x2.device, dtype=torch.float32)
+            p.colsum = colsum_out.data_ptr()
+    lib = _lib.load()
+    ws_b = lib.mc_linear_workspace_bytes(ctypes.byref(p))
+    if ws_b:
+        ws = _ws(ws_b, x2.device)
+        p.workspace, p.workspace_bytes = ws.data_ptr(), ws_b
+    _lib.check(lib.mc_linear(ctypes.byref(p), _lib.stream_handle(x2.device)), "mc_linear")
+    if epilogue == _lib.MC_LINEAR_EPI_BIAS_GELU:
+        return y, y2
+    if epilogue == _lib.MC_LINEAR_EPI_GELU_GRAD:
+        return y, colsum_out
+    return y
+
+
+# which MLP passes run on mc_linear (A/B toggles, tools/ab_step.py --toggle ops.MLP_HIP_FC1 ...):
+#   FC1: fc1 + bias + GELU in one epilogue; FC2: fc2 + bias; BWD: fc2's input gradient times GELU' with
+#   fc1's bias gradient in one epilogue, and fc1's input gradient.  Off: the library GEMM of that pass
+#   (+ the standalone GELU / mc_gelu_bwd passes).  Measured in DESIGN 4.3 (round 5).
+MLP_HIP_FC1 = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_FC1", "0") == "1"
+MLP_HIP_FC2 = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_FC2", "0") == "1"
+MLP_HIP_BWD = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_BWD", "0") == "1"
+
+
+def _gelu_bwd(h2, g2):
+    """(gh, db) = (g2 * gelu'(h2), column sums of gh) in one pass (mc_gelu_bwd)."""
+    lib = _lib.load()
+    V = 16 // h2.element_size()
+    cols = h2.shape[1]
+    h2, g2 = _hip_rows(h2, V, "gelu backward"), _hip_rows(g2, V, "gelu backward")
+    gh = torch.empty_like(h2)
+    db = torch.empty(cols, device=h2.device, dtype=torch.float32)
+    ws_b = lib.mc_grad_colsum_workspace_bytes(h2.shape[0], cols)
+    ws = _ws(ws_b, h2.device)
+    _lib.check(lib.mc_gelu_bwd(h2.shape[0], cols, _lib.dtype_code(h2.dtype), h2.data_ptr(), h2.stride(0),
+                               g2.data_ptr(), g2.stride(0), gh.data_ptr(), gh.stride(0), db.data_ptr(),
+                               ws.data_ptr(), ws_b, _lib.stream_handle(h2.device)), "mc_gelu_bwd")
+    return gh, db
+
+
+class MlpFn(torch.autograd.Function):
+    """y = fc2(gelu(fc1(x))) -- the ViT block's MLP (timm Mlp: fc1 -> nn.GELU() exact erf -> fc2; the
+    reference's image tower, model.py:1011-1017), each pass on mc_linear or the library per the
+    MLP_HIP_* toggles:
+      forward:  (h, a) = fc1 + bias + GELU in one epilogue;  y = a @ w2^T + b2
+      backward: gh = (gy @ w2) * gelu'(h) with fc1's bias gradient in one epilogue (no standalone
+                GELU-backward pass, no stored fc2 input gradient);  dx = gh @ w1;  dW1, dW2 on
+                mc_gemm_wgrad;  db2 = column sums of gy.
+    Same roundings as the unfused chain: h, a, y, ga (inside the epilogue) and gh once each in the
+    activation dtype."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        dt = _compute_dtype(x)
+        xc = x.to(dt)
+        w1c, b1c, w2c, b2c = _wcast(w1, dt), _wcast(b1, dt), _wcast(w2, dt), _wcast(b2, dt)
+        x2 = xc.reshape(-1, xc.shape[-1])
+        with torch.autocast("cuda", enabled=False):
+            if MLP_HIP_FC1:
+                h, a = linear_hip(x2, w1c, b1c, _lib.MC_LINEAR_EPI_BIAS_GELU)
+            else:
+                h = torch.nn.functional.linear(x2, w1c, b1c)
+                a = torch.nn.functional.gelu(h)
+            y = linear_hip(a, w2c, b2c) if MLP_HIP_FC2 else torch.nn.functional.linear(a, w2c, b2c)
+        ctx.save_for_backward(x2, h, a, w1c, w2c)
+        ctx.wt1, ctx.wt2 = _wcast_t(w1, xc, dt), _wcast_t(w2, a, dt)
+        ctx.xshape = xc.shape
+        return y.view(*xc.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, h, a, w1c, w2c = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1]).to(h.dtype)
+        if not _aligned_rows(g2, 8):
+            g2 = g2.contiguous()
+        pre = getattr(gy, COLSUM_ATTR, None)   # gy's column sums taken by its producer (LayerNorm bwd)
+        if pre is not None and pre[1] == gy._version and pre[0].shape[0] == g2.shape[1]:
+            db2 = pre[0]
+        else:
+            db2 = colsum(g2)
+        dw2 = wgrad(g2.t(), a)
+        if MLP_HIP_BWD:
+            wt2 = ctx.wt2 if ctx.wt2 is not None else w2c.t().contiguous()
+            gh, db1 = linear_hip(g2, wt2, None, _lib.MC_LINEAR_EPI_GELU_GRAD, h=h, want_colsum=True)
+        else:
+            gh, db1 = _gelu_bwd(h, _dgrad(g2, w2c, ctx.wt2))
+        dw1 = wgrad(gh.t(), x2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if MLP_HIP_BWD:
+                wt1 = ctx.wt1 if ctx.wt1 is not None else w1c.t().contiguous()
+                dx = linear_hip(gh, wt1)
+            else:
+                dx = _dgrad(gh, w1c, ctx.wt1)
+            dx = dx.view(ctx.xshape)
+        return dx, dw1, db1, dw2, db2
+
+
+def mlp_hip_ok(x, w1, b1, w2, b2):
+    """The ViT MLP qualifies for MlpFn: on the GPU, 16-bit compute, biases, widths % 64 (both GEMMs' K)."""
+    dt = _compute_dtype(x)
+    return (x.is_cuda and b1 is not None and b2 is not None and dt in (torch.bfloat16, torch.float16) and w1.dim() == 2 and w2.dim() == 2
+            and x.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0 and w2.shape[0] % 64 == 0
+            and x.numel() // max(x.shape[-1], 1) >= 1)
+
+
+def mlp(x, w1, b1, w2, b2):
+    """ViT MLP y = fc2(gelu(fc1(x))): MlpFn on the GPU, else fc1_gelu + linear_sk."""
+    if (MLP_HIP_FC1 or MLP_HIP_FC2 or MLP_HIP_BWD) and mlp_hip_ok(x, w1, b1, w2, b2):
+        return MlpFn.apply(x, w1, b1, w2, b2)
+    return linear_sk(fc1_gelu(x, w1, b1), w2, b2)
+
+
 class FC1GeluFn(torch.autograd.Function):
     """a = gelu(x @ w^T + b) -- the MLP's first projection and activation (timm Mlp fc1 + GELU).
 

@@ -45,3 +45,14 @@ print(f"one training step, all queues: kernels {len(seq)}  kernel-busy sum {busy
 print("busy per queue: " + ", ".join(f"queue {q}: {t / 1e3:.2f} ms" for q, t in sorted(per_queue.items())))
 for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
     print(f"{t / 1e3:8.2f} ms  {c:5d}  {t / c:9.1f} us  {n}")
+qagg = defaultdict(lambda: defaultdict(lambda: [0, 0.0]))
+for r in seq:
+    n = re.sub(r"void |at::native::|\(anonymous namespace\)::", "", r["Kernel_Name"])[:110]
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    e = qagg[r.get("Queue_Id", "?")][n]
+    e[0] += 1
+    e[1] += d
+for q, kern in sorted(qagg.items()):
+    print(f"\nqueue {q}: busy {per_queue[q] / 1e3:.2f} ms")
+    for n, (c, t) in sorted(kern.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"{t / 1e3:8.2f} ms  {c:5d}  {t / c:9.1f} us  {n}")
