@@ -1317,10 +1317,12 @@ def linear_hip(x2, w, bias=None, epilogue=None, h=None, want_colsum=False):
 # which MLP passes run on mc_linear (A/B toggles, tools/ab_step.py --toggle ops.MLP_HIP_FC1 ...):
 #   FC1: fc1 + bias + GELU in one epilogue; FC2: fc2 + bias; BWD: fc2's input gradient times GELU' with
 #   fc1's bias gradient in one epilogue, and fc1's input gradient.  Off: the library GEMM of that pass
-#   (+ the standalone GELU / mc_gelu_bwd passes).  Measured in DESIGN 4.3 (round 5).
+#   (+ the standalone GELU / mc_gelu_bwd passes).  Measured in DESIGN 4.3 (round 5, same-box C2 step
+#   A/B, profiles/r05/linear/): BWD -0.35..-0.52 ms (4 of 4 reps), FC2 -0.04..-0.35 ms (3 of 3) -- on;
+#   FC1 +0.07..+0.44 ms (its un-overlapped GELU epilogue costs more than the pass it saves) -- off.
 MLP_HIP_FC1 = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_FC1", "0") == "1"
-MLP_HIP_FC2 = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_FC2", "0") == "1"
-MLP_HIP_BWD = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_BWD", "0") == "1"
+MLP_HIP_FC2 = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_FC2", "1") == "1"
+MLP_HIP_BWD = os.environ.get("MAMBA_CLIP_AMD_MLP_HIP_BWD", "1") == "1"
 
 
 def _gelu_bwd(h2, g2):
