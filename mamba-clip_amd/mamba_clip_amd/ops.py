@@ -1054,8 +1054,25 @@ DGRAD_TN = os.environ.get("MAMBA_CLIP_AMD_DGRAD_TN", "1") != "0"
 WCAST_T = os.environ.get("MAMBA_CLIP_AMD_WCAST_T", "1") != "0"     # A/B: scope copies vs per-call transposes
 
 
+# The remaining towers' Linear forward / input-gradient GEMMs (qkv, proj, patch embedding, the MLP's
+# fc1 input gradient) on mc_linear instead of the library: A/B toggles.
+LINEAR_HIP_FWD = os.environ.get("MAMBA_CLIP_AMD_LINEAR_HIP_FWD", "0") == "1"
+LINEAR_HIP_DGRAD = os.environ.get("MAMBA_CLIP_AMD_LINEAR_HIP_DGRAD", "0") == "1"
+
+
+def _fwd_gemm(xc, wc, bc):
+    """F.linear(xc, wc, bc), on mc_linear (bias epilogue) when LINEAR_HIP_FWD and the shapes qualify."""
+    if LINEAR_HIP_FWD and xc.is_cuda and xc.dim() >= 2 and (bc is None or bc.dtype == xc.dtype):
+        x2 = xc.reshape(-1, xc.shape[-1])
+        if x2.shape[0] >= 8192 and linear_hip_ok(x2, wc):
+            return linear_hip(x2, wc, bc).view(*xc.shape[:-1], wc.shape[0])
+    return torch.nn.functional.linear(xc, wc, bc)
+
+
 def _dgrad(g2, wc, wt=None):
     """g2 (M, N) @ wc (N, K) for a row-major weight copy wc (wt: its transposed copy, or None)."""
+    if LINEAR_HIP_DGRAD and wt is not None and g2.shape[0] >= 8192 and linear_hip_ok(g2, wt):
+        return linear_hip(g2, wt)
     if wt is not None:
         return torch.mm(g2, wt.t())
     if DGRAD_TN and g2.is_cuda and g2.shape[0] >= 8192 and wc.shape[0] * wc.shape[1] >= 1 << 19:
@@ -1078,7 +1095,7 @@ class LinearSK(torch.autograd.Function):
         xc, wc = x.to(dt), _wcast(weight, dt)
         bc = _wcast(bias, dt) if bias is not None else None
         with torch.autocast("cuda", enabled=False):
-            y = torch.nn.functional.linear(xc, wc, bc)
+            y = _fwd_gemm(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.has_bias = bias is not None
         colmajor = xc.dim() == 2 and xc.stride(0) == 1 and xc.stride(1) != 1
@@ -1475,7 +1492,7 @@ class QKVProjFn(torch.autograd.Function):
         xc, wc, bc = x.to(dt), _wcast(weight, dt), _wcast(bias, dt)
         Bsz, N, C = xc.shape
         with torch.autocast("cuda", enabled=False):
-            y = torch.nn.functional.linear(xc, wc, bc)
+            y = _fwd_gemm(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.heads = heads
         ctx.wt = _wcast_t(weight, xc, dt)
