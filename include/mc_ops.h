@@ -248,6 +248,9 @@ int mc_mixer_proj_bwd(const mc_mixer_proj_bwd_params* p, void* stream);
 size_t mc_colsum_workspace_bytes(int32_t rows, int32_t cols);
 int mc_colsum(int32_t rows, int32_t cols, int32_t dtype, const void* x, int64_t ld, float* out,
               void* workspace, size_t workspace_bytes, void* stream);
+/* out[c] = sum_k part[k * cols + c] (fp32), k = 0 .. nslices-1, in a fixed order: the fold of per-slice /
+ * per-tile column partials (e.g. mc_linear's GELU' epilogue, one row per 256-token tile). */
+int mc_colsum_fold(int32_t nslices, int32_t cols, const float* part, float* out, void* stream);
 
 /* mc_l2norm_fwd / _bwd: torch.nn.functional.normalize(x, dim=-1) for a (rows, cols) matrix -- the
  * features ClipModel.encode_image / encode_text(normalize=True) return (reference model.py:1011-1017).

@@ -33,6 +33,7 @@
 #include "../../include/mc_gemm.h"
 
 extern "C" int mc_sum_slabs(int32_t s, int64_t n, const float* src, int64_t slab_stride, float* dst, void* stream);
+extern "C" int mc_colsum_fold(int32_t nslices, int32_t cols, const float* part, float* out, void* stream);
 
 namespace mc {
 namespace wgrad {
@@ -773,6 +774,7 @@ extern "C" int mc_linear(const mc_linear_params* p, void* stream) {
   else launch_linear<f16_t>(a, p->epilogue, s);
   hipError_t e = hipGetLastError();
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_linear: launch failed: %s", hipGetErrorString(e));
-  if (sums) return mc_sum_slabs(tiles_n, p->cols, a.colpart, p->cols, p->colsum, stream);
+  // the per-tile partial rows: many (197 at C2) short rows -> the slice fold, 8 slices in flight per column
+  if (sums) return mc_colsum_fold(tiles_n, p->cols, a.colpart, p->colsum, stream);
   return MC_OK;
 }

@@ -1590,3 +1590,14 @@ extern "C" int mc_l2norm_bwd(int32_t rows, int32_t cols, int32_t dtype, const vo
                                           (T*)dx, lddx));
   return check_launch("mc_l2norm_bwd");
 }
+
+// out[c] = sum over k of part[k][c], in a fixed order (colsum_slices_kernel): the fold of per-tile /
+// per-slice column partials (mc_linear's GELU' epilogue writes one row per 256-token tile).
+extern "C" int mc_colsum_fold(int32_t nslices, int32_t cols, const float* part, float* out, void* stream) {
+  MC_CHECK(nslices >= 1 && cols >= 0, MC_ERR_SHAPE, "mc_colsum_fold: bad shape (nslices %d, cols %d)", nslices, cols);
+  if (cols == 0) return MC_OK;
+  MC_CHECK(part && out, MC_ERR_INVALID, "mc_colsum_fold: null pointer");
+  hipLaunchKernelGGL(colsum_slices_kernel, dim3((cols + 31) / 32), dim3(256), 0, (hipStream_t)stream, part, nslices, cols,
+                     out);
+  return check_launch("mc_colsum_fold");
+}

@@ -292,6 +292,7 @@ SYMBOLS = {
     "mc_adamw_step": (ctypes.c_int, [c_i32, c_vp, c_vp, ctypes.POINTER(AdamWHyper), c_vp]),
     "mc_sum_slabs": (ctypes.c_int, [c_i32, c_i64, c_fp, c_i64, c_fp, c_vp]),
     "mc_colsum_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "mc_colsum_fold": (ctypes.c_int, [c_i32, c_i32, c_fp, c_fp, c_vp]),
     "mc_colsum": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_fp, c_vp, ctypes.c_size_t, c_vp]),
     "mc_l2norm_fwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, ctypes.c_float, c_fp, c_i64, c_fp, c_vp]),
     "mc_l2norm_bwd": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_fp, ctypes.c_float, c_fp, c_i64, c_vp,
