@@ -550,11 +550,13 @@ __device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4
       if (!fok || t >= g.N) continue;
       float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float phi, pdf;
-        const float x = elem_f<T>(hq[p], e);
-        phi_pdf_f(x, phi, pdf);
-        o[e] = elem_f<T>(q, e) * fmaf(x, pdf, phi);
+      for (int e = 0; e < 8; e += 2) {
+        f32x2 phi, pdf;
+        const f32x2 x = f32x2{elem_f<T>(hq[p], e), elem_f<T>(hq[p], e + 1)};
+        phi_pdf_f2(x, phi, pdf);
+        const f32x2 gr = x * pdf + phi;   // gelu'(x), torch's cdf + x * pdf
+        o[e] = elem_f<T>(q, e) * gr.x;
+        o[e + 1] = elem_f<T>(q, e + 1) * gr.y;
       }
       const uint4 oq = pack_f<T>(o);
       st16(reinterpret_cast<T*>(g.Y) + (int64_t)t * g.ldy + f, oq);

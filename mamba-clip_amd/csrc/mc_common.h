@@ -253,6 +253,30 @@ __device__ __forceinline__ void phi_pdf_f(float x, float& phi, float& pdf) {
   pdf = 0.39894228040143268f * e;
 }
 
+// phi_pdf_f on two values at once: the fit's FMAs as packed v_pk_fma_f32 (half the issue slots)
+__device__ __forceinline__ void phi_pdf_f2(f32x2 x, f32x2& phi, f32x2& pdf) {
+  const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const f32x2 d = z * 0.5f + 1.f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = f32x2{0.17087277f, 0.17087277f};
+  p = p * t + -0.82215223f;
+  p = p * t + 1.48851587f;
+  p = p * t + -1.13520398f;
+  p = p * t + 0.27886807f;
+  p = p * t + -0.18628806f;
+  p = p * t + 0.09678418f;
+  p = p * t + 0.37409196f;
+  p = p * t + 1.00002368f;
+  p = p * t + -1.26551223f;
+  const f32x2 ea = x * x * -0.72134752044448170f;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  const f32x2 pl = p * 1.4426950408889634f;
+  const f32x2 erf_abs = 1.f - t * e * f32x2{__builtin_amdgcn_exp2f(pl.x), __builtin_amdgcn_exp2f(pl.y)};
+  const f32x2 erf_x = f32x2{x.x < 0.f ? -erf_abs.x : erf_abs.x, x.y < 0.f ? -erf_abs.y : erf_abs.y};
+  phi = (erf_x + 1.f) * 0.5f;
+  pdf = e * 0.39894228040143268f;
+}
+
 // ---------------------------------------------------------------- host error plumbing
 void set_error(const char* fmt, ...);
 const char* last_error();
