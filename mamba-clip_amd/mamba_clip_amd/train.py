@@ -263,18 +263,21 @@ class GraphedStep:
         dt = torch.bfloat16 if args.precision in ("amp_bf16", "amp_bfloat16") else torch.float16
         return lambda: torch.autocast("cuda", dtype=dt, cache_enabled=False)
 
-    def __init__(self, model, images, texts, targets, loss, optimizer, args, warmup=3):
+    def __init__(self, model, images, texts, targets, loss, optimizer, args, warmup=3, concurrent=False):
         if getattr(args, "balanced_mixup", None):
             # the mixup draws lam (and the lam > 0.5 text swap) on the host: a replay would repeat the
             # capture's draw forever
             raise ValueError("GraphedStep: balanced_mixup draws host-side randomness per step; run it eager")
         autocast = self.autocast_for(args)
         inner = unwrap_model(model)
-        # one stream: the towers' two-stream fork / join does not survive capture race-free here (replays
-        # of a two-stream capture differed run to run in round 4's test); replay order = eager order.
-        # The flag is restored after the capture, so later eager steps run the towers concurrently again.
+        # One stream by default: replay order = eager order, and the replays are bitwise repeatable.
+        # concurrent=True captures the towers' two-stream fork / join as two graph branches (round 5:
+        # with the glue reductions deterministic, DESIGN 4.9, the replays match the eager two-stream step
+        # to the tolerance below; tests/test_graph_gpu.py).  The flag is restored after the capture, so
+        # later eager steps run the towers concurrently again.
         prev = getattr(inner, "concurrent_towers", False)
-        inner.concurrent_towers = False
+        if not concurrent:
+            inner.concurrent_towers = False
         run = lambda: train_step(model, images, texts, targets, loss, optimizer, None, args, autocast)  # noqa: E731
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())

@@ -42,3 +42,34 @@ def test_graphed_step_matches_eager(model_name, batch):
         assert abs(e - g) <= 1e-3 * abs(e) + 1e-4, (eager, graphed)
     for (n, p0), p1 in zip(m0.named_parameters(), m1.parameters()):
         assert float((p0 - p1).abs().max()) <= 1e-2 * float(p0.abs().max()) + 1e-6, n
+
+
+
+def test_two_stream_graphed_step_tracks_eager():
+    """The towers' two-stream fork / join captured as two graph branches (GraphedStep(concurrent=True))
+    replays and tracks the eager two-stream step.  Not to the one-stream capture's 1e-3: at this batch the
+    eager two-stream step itself is not run-to-run reproducible with several hardware queues (two eager
+    runs measured 1.4654 vs 1.4669 at step 4: the Mamba tower's scan-backward parameter gradients, DESIGN
+    4.9), so the replays are held to 1e-2 relative on the loss and 2e-2 (+ AdamW's 2 lr per step) on the
+    parameters.  (With one
+    hardware queue, where the eager step is reproducible, capturing the two branches ended the process
+    with SIGSEGV inside the runtime: not used.)"""
+    from mamba_clip_amd.train import GraphedStep, train_step
+    m0, o0, l0, a0, (img, txt, tgt) = _setup("vit_b16-mamba130m", 8, 11)
+    m0.concurrent_towers = True
+    assert m0._side_stream(img, txt) is not None, "the towers do not run on two streams at this shape"
+    eager = []
+    for _ in range(6):
+        eager.append(float(train_step(m0, img, txt, tgt, l0, o0, None, a0, GraphedStep.autocast_for(a0))["loss"].detach()))
+    m1, o1, l1, a1, (img1, txt1, tgt1) = _setup("vit_b16-mamba130m", 8, 11)
+    m1.concurrent_towers = True
+    step = GraphedStep(m1, img1, txt1, tgt1, l1, o1, a1, warmup=3, concurrent=True)
+    assert m1.concurrent_towers
+    graphed = [float(step()["loss"].detach()) for _ in range(3)]
+    for e, g in zip(eager[3:], graphed):
+        assert abs(e - g) <= 1e-2 * abs(e) + 1e-4, (eager, graphed)
+    # AdamW moves every element by up to lr per step whatever its gradient's size, so a near-zero
+    # gradient that differs in sign moves an element 2 lr apart (the zero-initialised biases): the
+    # parameters are held to 2e-2 of their scale plus 2 lr per step
+    for (n, p0), p1 in zip(m0.named_parameters(), m1.parameters()):
+        assert float((p0 - p1).abs().max()) <= 2e-2 * float(p0.abs().max()) + 2 * a0.lr * 6, n
