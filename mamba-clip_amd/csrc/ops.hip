@@ -133,6 +133,31 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(int rows, int cols
   }
 }
 
+// The 4 waves of a block fold their per-lane column partials in LDS in a fixed order (wave 0 + 1 + 2 + 3)
+// and wave 0 writes ONE partial row per block: the column-sum passes then read kNormGrid rows, not
+// 4 kNormGrid.  Every wave of the block must call it (it holds two barriers per vector).
+template <int NV, int V>
+__device__ __forceinline__ void block_fold_store(const float (&acc)[NV][V], int lane, int nvec, float* __restrict__ dst) {
+  __shared__ float red[3][64 * V];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = lane + 64 * i;
+    if (w > 0) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) red[w - 1][lane * V + e] = acc[i][e];
+    }
+    __syncthreads();
+    if (w == 0 && v < nvec) {
+      float o[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) o[e] = ((acc[i][e] + red[0][lane * V + e]) + red[1][lane * V + e]) + red[2][lane * V + e];
+      st_f32v<V>(dst + v * V, o);
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                               const float* __restrict__ dres,
@@ -194,11 +219,7 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(int rows, int cols
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < nvec) st_f32v<V>(dw_part + (int64_t)wave * cols + v * V, dwacc[i]);
-  }
+  block_fold_store<NV, V>(dwacc, lane, nvec, dw_part + (int64_t)blockIdx.x * cols);
 }
 
 // Deterministic column sums of a row-major partial slab in two passes:
@@ -350,8 +371,8 @@ __global__ __launch_bounds__(256) void add_layernorm_fwd_kernel(int rows, int co
 }
 
 // dh_total = dh + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
-// dx (= dres) = dh_total;  part rows: [wave][0..cols) dw, [wave][cols..2cols) db and, with kDxSum,
-// [wave][2cols..3cols) the column sums of dx as stored: the bias gradient of the layer whose output
+// dx (= dres) = dh_total;  part rows (one per block, its 4 waves folded in order): [block][0..cols) dw, [block][cols..2cols) db and, with kDxSum,
+// [block][2cols..3cols) the column sums of dx as stored: the bias gradient of the layer whose output
 // entered as x (fc2 / attention proj), taken in this pass instead of a second read of dx
 template <typename T, int NV, bool kDxSum>
 __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
@@ -449,16 +470,11 @@ __global__ __launch_bounds__(256) void add_layernorm_bwd_kernel(int rows, int co
       }
     }
   }
-  constexpr int kW = kDxSum ? 3 : 2;   // partial columns per wave
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < nvec) {
-      st_f32v<V>(part + (int64_t)wave * kW * cols + v * V, dwacc[i]);
-      st_f32v<V>(part + (int64_t)wave * kW * cols + cols + v * V, dbacc[i]);
-      if constexpr (kDxSum) st_f32v<V>(part + (int64_t)wave * kW * cols + 2 * cols + v * V, dxacc[i]);
-    }
-  }
+  constexpr int kW = kDxSum ? 3 : 2;   // partial columns per block row
+  float* row = part + (int64_t)blockIdx.x * kW * cols;
+  block_fold_store<NV, V>(dwacc, lane, nvec, row);
+  block_fold_store<NV, V>(dbacc, lane, nvec, row + cols);
+  if constexpr (kDxSum) block_fold_store<NV, V>(dxacc, lane, nvec, row + 2 * cols);
 }
 
 // vectors per lane per row -> template instance
@@ -1076,7 +1092,7 @@ extern "C" int mc_add_rmsnorm_bwd(int32_t rows, int32_t cols, int32_t dtype, con
   float* part = reinterpret_cast<float*>(workspace);
   MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_rmsnorm_bwd_kernel<T, NV>),
       dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, dres, h, w, rstd, (T*)dx, dres_in, part)));
-  colsum_two_pass(part, kNormGrid * 4, cols, cols, dw, nullptr, part + (size_t)kNormGrid * 4 * cols, s);
+  colsum_two_pass(part, kNormGrid, cols, cols, dw, nullptr, part + (size_t)kNormGrid * 4 * cols, s);
   return check_launch("mc_add_rmsnorm_bwd");
 }
 
@@ -1126,8 +1142,8 @@ extern "C" int mc_add_layernorm_bwd(int32_t rows, int32_t cols, int32_t dtype, c
     MC_DISPATCH_T(dtype, MC_DISPATCH_NV(norm_nv(cols, V), hipLaunchKernelGGL((add_layernorm_bwd_kernel<T, NV, false>),
         dim3(kNormGrid), dim3(256), 0, s, rows, cols, (const T*)dy, (const T*)dh, (const T*)h, w, mean, rstd, (T*)dx,
         part)));
-  // part is [wave][kw * cols]: dw in columns [0, cols), dbias in [cols, 2 cols), dx sums in [2 cols, 3 cols)
-  colsum_two_pass(part, kNormGrid * 4, kw * cols, cols, dw, dbias, part + (size_t)kNormGrid * 4 * kw * cols, s,
+  // part is [block][kw * cols]: dw in columns [0, cols), dbias in [cols, 2 cols), dx sums in [2 cols, 3 cols)
+  colsum_two_pass(part, kNormGrid, kw * cols, cols, dw, dbias, part + (size_t)kNormGrid * 4 * kw * cols, s,
                   dx_colsum);
   return check_launch("mc_add_layernorm_bwd");
 }
