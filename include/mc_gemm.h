@@ -96,6 +96,16 @@ typedef struct mc_linear_params {
 size_t mc_linear_workspace_bytes(const mc_linear_params* p);
 int mc_linear(const mc_linear_params* p, void* stream);
 
+/*
+ * mc_gemm_small_k: Y (M x T) = W (M x K) X (K x T), 16-bit, fp32 accumulation, one rounding -- a short
+ * reduction (K in {16, 32, 48, 64}) over rows of X with unit token stride: the Mamba mixer's dt_proj
+ * forward, delta = W_dt dt_raw (reference: Mamba's dt_proj Linear applied to x_proj's dt rows; the SS2D
+ * form is the einsum at model.py:519-528).  W rows 8-B aligned (ldw % 4 == 0), X / Y rows 16-B aligned
+ * (ldx % 8, ldy % 8 == 0), T % 8 == 0.
+ */
+int mc_gemm_small_k(int32_t M, int32_t K, int32_t T, int32_t dtype, const void* W, int64_t ldw, const void* X,
+                    int64_t ldx, void* Y, int64_t ldy, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -780,3 +780,123 @@ extern "C" int mc_linear(const mc_linear_params* p, void* stream) {
   if (sums) return mc_colsum_fold(tiles_n, p->cols, a.colpart, p->colsum, stream);
   return MC_OK;
 }
+
+// ------------------------------------------------------------------ mc_gemm_small_k
+// Y (M x T) = W (M x K) X (K x T) for a short reduction (K <= 64, K % 16 == 0) and a long, unit-stride
+// token dimension: the Mamba mixer's dt_proj forward, delta = W_dt dt_raw (reference model.py:519-528:
+// the einsum with dt_projs_weight; Mamba's dt_proj Linear) -- the library runs it at ~1/3 of the
+// output-write rate.  One workgroup = 256 tokens x 64 rows of Y; X's K x 256 tile is staged in LDS
+// (rows padded to 544 B: the transposed reads of 8 rows hit distinct banks) and read back as MFMA A
+// operands with ds_read_b64_tr_b16 (the k-strided direction); W's rows are the B operands straight
+// from global memory (8-B pieces, L2-resident); the Y^T tiles (4 consecutive tokens per lane) are
+// staged back through the LDS and leave as whole 512-B row pieces.  v_mfma_f32_16x16x16_{bf16,f16}, fp32 accumulation, one rounding.
+namespace mc {
+namespace skinny {
+constexpr int kTT = 256, kTM = 64, kRow = 544;   // tokens / rows per workgroup, LDS row bytes
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(s16x4_t a, s16x4_t b, f32x4 c) {
+  if constexpr (std::is_same<T, bf16_t>::value) return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+  else {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b), c, 0, 0, 0);
+  }
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(256) void small_k_kernel(int M, int Tn, const T* __restrict__ W, int64_t ldw,
+                                                      const T* __restrict__ X, int64_t ldx, T* __restrict__ Y,
+                                                      int64_t ldy) {
+  constexpr int kORow = 528;   // output image row: 256 tokens + 16 B pad (the 16 rows of a store hit distinct banks)
+  constexpr int kLds = K * kRow > kTM * kORow ? K * kRow : kTM * kORow;
+  __shared__ __attribute__((aligned(16))) char xs[kLds];   // X tile, then the output tile
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_t = (Tn + kTT - 1) / kTT;
+  const int t0 = (blockIdx.x % tiles_t) * kTT, m0 = (blockIdx.x / tiles_t) * kTM;
+  // X tile -> LDS: K rows x 256 tokens, 16-B vectors (tokens past Tn read as 0)
+  constexpr int kVecs = K * kTT / 8;
+#pragma unroll
+  for (int j = 0; j < (kVecs + 255) / 256; ++j) {
+    const int q = tid + 256 * j;
+    if (q < kVecs) {
+      const int r = q / (kTT / 8), c = (q % (kTT / 8)) * 8;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (t0 + c < Tn) v = ld16(X + (int64_t)r * ldx + t0 + c);   // Tn % 8 == 0: whole vectors
+      *reinterpret_cast<uint4*>(xs + r * kRow + c * 2) = v;
+    }
+  }
+  // B operands: W[m0 + 16 cb + i][16 kk + 4 g .. + 3] (rows past M clamped; their columns are not stored)
+  const int g = lane >> 4, i = lane & 15;
+  s16x4_t bfr[4][K / 16];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int m = min(m0 + 16 * cb + i, M - 1);
+#pragma unroll
+    for (int kk = 0; kk < K / 16; ++kk)
+      bfr[cb][kk] = *reinterpret_cast<const s16x4_t*>(W + (int64_t)m * ldw + 16 * kk + 4 * g);
+  }
+  __syncthreads();
+  // A operands by transposed reads: lane 4q + p of group g addresses row 16 kk + 4 g + q, tokens tb + 4 p
+  const int q = i >> 2, p = i & 3;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[tb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < K / 16; ++kk)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb) {
+      const int tl = w * 64 + tb * 16 + 4 * p;
+      const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4_t*)((__attribute__((address_space(3))) char*)(xs) + (16 * kk + 4 * g + q) * kRow + tl * 2));
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[tb][cb] = mfma16<T>(a, bfr[cb][kk], acc[tb][cb]);
+    }
+  // C (16 tokens x 16 rows): lane holds tokens 4 g .. 4 g + 3 of row i -> the LDS output image
+  // [64 rows][256 tokens], then whole 512-B row pieces of Y (16-B stores, a wave per two rows)
+  __syncthreads();   // every wave's transposed reads of the X tile are done
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const f32x4 v = acc[tb][cb];
+      *reinterpret_cast<uint2*>(xs + (16 * cb + i) * kORow + (w * 64 + tb * 16 + 4 * g) * 2) =
+          make_uint2(cvt_pk2<T>(v[0], v[1]), cvt_pk2<T>(v[2], v[3]));
+    }
+  __syncthreads();
+  const int cv = tid & 31, rr = tid >> 5;
+#pragma unroll
+  for (int j = 0; j < kTM / 8; ++j) {
+    const int r = 8 * j + rr, m = m0 + r, t = t0 + cv * 8;
+    if (m < M && t < Tn) st16(Y + (int64_t)m * ldy + t, *reinterpret_cast<const uint4*>(xs + r * kORow + cv * 16));
+  }
+}
+}  // namespace skinny
+}  // namespace mc
+
+extern "C" int mc_gemm_small_k(int32_t M, int32_t K, int32_t T, int32_t dtype, const void* W, int64_t ldw, const void* X,
+                               int64_t ldx, void* Y, int64_t ldy, void* stream) {
+  MC_CHECK(dtype == MC_DTYPE_BF16 || dtype == MC_DTYPE_F16, MC_ERR_DTYPE, "mc_gemm_small_k: bf16 / f16 only");
+  MC_CHECK(M > 0 && T >= 0 && (K == 16 || K == 32 || K == 48 || K == 64) && T % 8 == 0, MC_ERR_SHAPE,
+           "mc_gemm_small_k: M %d > 0, K %d in {16, 32, 48, 64}, T %d %% 8 == 0", M, K, T);
+  MC_CHECK(W && X && Y && aligned16(X) && aligned16(Y) && (reinterpret_cast<uintptr_t>(W) & 7) == 0 && ldw % 4 == 0 &&
+               ldw >= K && ldx % 8 == 0 && ldx >= T && ldy % 8 == 0 && ldy >= T,
+           MC_ERR_SHAPE, "mc_gemm_small_k: 16-B aligned X / Y rows (ld %% 8), 8-B aligned W rows");
+  if (T == 0) return MC_OK;
+  const dim3 grid(((T + skinny::kTT - 1) / skinny::kTT) * ((M + skinny::kTM - 1) / skinny::kTM)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define MC_SMALLK(TT, KK) hipLaunchKernelGGL((skinny::small_k_kernel<TT, KK>), grid, block, 0, s, M, T, (const TT*)W, ldw, \
+                                             (const TT*)X, ldx, (TT*)Y, ldy)
+  if (dtype == MC_DTYPE_BF16) {
+    if (K == 16) MC_SMALLK(bf16_t, 16); else if (K == 32) MC_SMALLK(bf16_t, 32); else if (K == 48) MC_SMALLK(bf16_t, 48); else MC_SMALLK(bf16_t, 64);
+  } else {
+    if (K == 16) MC_SMALLK(f16_t, 16); else if (K == 32) MC_SMALLK(f16_t, 32); else if (K == 48) MC_SMALLK(f16_t, 48); else MC_SMALLK(f16_t, 64);
+  }
+#undef MC_SMALLK
+  hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_small_k: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}

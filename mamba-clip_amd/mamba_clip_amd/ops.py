@@ -1134,6 +1134,29 @@ def linear_sk(x, weight, bias=None):
     return LinearSK.apply(x, weight, bias)
 
 
+# w @ X with a short reduction (the mixer's dt_proj forward, K = dt_rank) on mc_gemm_small_k instead of
+# the library GEMM.  A/B toggle.
+SMALL_K_HIP = os.environ.get("MAMBA_CLIP_AMD_SMALL_K_HIP", "1") != "0"
+
+
+def small_k_ok(wc, Xc):
+    K = wc.shape[1]
+    return (SMALL_K_HIP and Xc.is_cuda and wc.dtype == Xc.dtype and Xc.dtype in (torch.bfloat16, torch.float16)
+            and K in (16, 32, 48, 64) and Xc.shape[1] % 8 == 0 and Xc.stride(1) == 1 and Xc.stride(0) % 8 == 0
+            and Xc.data_ptr() % 16 == 0 and wc.stride(1) == 1 and wc.stride(0) % 4 == 0 and wc.data_ptr() % 8 == 0)
+
+
+def gemm_small_k(wc, Xc):
+    """wc (M, K) @ Xc (K, T) on mc_gemm_small_k (caller checks small_k_ok)."""
+    M, K = wc.shape
+    T = Xc.shape[1]
+    y = torch.empty(M, T, device=Xc.device, dtype=Xc.dtype)
+    _lib.check(_lib.load().mc_gemm_small_k(M, K, T, _lib.dtype_code(Xc.dtype), wc.data_ptr(), wc.stride(0),
+                                           Xc.data_ptr(), Xc.stride(0), y.data_ptr(), T,
+                                           _lib.stream_handle(Xc.device)), "mc_gemm_small_k")
+    return y
+
+
 class WeightLeftMM(torch.autograd.Function):
     """y = w @ X for a weight w (N, K) and activations X (K, M) (channel-major GEMMs of the Mamba mixer)."""
 
@@ -1142,7 +1165,7 @@ class WeightLeftMM(torch.autograd.Function):
         dt = _compute_dtype(X)
         wc, Xc = _wcast(weight, dt), X.to(dt)
         with torch.autocast("cuda", enabled=False):
-            y = torch.mm(wc, Xc)
+            y = gemm_small_k(wc, Xc) if small_k_ok(wc, Xc) else torch.mm(wc, Xc)
         ctx.save_for_backward(wc, Xc)
         ctx.handoff = handoff
         ctx.out_slab = out_slab   # (GradSlab, first row): dX written into those rows (ops.GradSlab)

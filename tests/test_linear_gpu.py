@@ -172,3 +172,21 @@ def test_mlp_fn_bitwise_repeatable(mlp_all_hip):
         y.backward(gy)
         runs.append([y.detach(), x.grad] + [p.grad.clone() for p in (*fc1.parameters(), *fc2.parameters())])
     assert all(torch.equal(a, b) for a, b in zip(*runs))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K,T", [(1536, 48, 20480), (1536, 48, 640), (3072, 64, 2056), (100, 16, 256), (48, 32, 8)])
+def test_gemm_small_k(M, K, T, dt):
+    """mc_gemm_small_k (the mixer's dt_proj forward) vs an fp64 product of the same operands; X a row view
+    of a wider buffer (the x_dbl slab's dt rows), ragged M and T."""
+    g = torch.Generator(device=DEV).manual_seed(M + K + T)
+    w = _rand((M, K), dt, g, 0.2)
+    xb = _rand((K + 32, T), dt, g)
+    x = xb[:K]                                                 # dt rows of a (R + 2N, T) slab
+    assert ops.small_k_ok(w, x)
+    y = ops.gemm_small_k(w, x)
+    ref = w.double() @ x.double()
+    bound = (w.double().abs() @ x.double().abs()) * 1e-5 + ref.abs() * ULP[dt] / 2 + 1e-6
+    err = (y.double() - ref).abs()
+    assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
+    assert torch.equal(y, ops.gemm_small_k(w, x))

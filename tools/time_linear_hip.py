@@ -104,7 +104,23 @@ def epilogues():
                           "hip_gemm_tflops": round(flop / hip_us / 1e6, 1)}), flush=True)
 
 
+def small_k():
+    """mc_gemm_small_k vs torch.mm at the C2 dt_proj forward: (1536 x 48) @ (48 x 20480) rows of the x_dbl slab."""
+    g = torch.Generator(device=DEV).manual_seed(2)
+    bf = torch.bfloat16
+    w = ((torch.rand(1536, 48, device=DEV, generator=g) * 2 - 1) * 0.1).to(bf)
+    slab = (torch.rand(80, 20480, device=DEV, generator=g) * 2 - 1).to(bf)
+    x = slab[:48]
+    lib_us, hip_us = timed(lambda: torch.mm(w, x)), timed(lambda: ops.gemm_small_k(w, x))
+    nbytes = 1536 * 20480 * 2 + 48 * 20480 * 2
+    print(json.dumps({"case": "dt_proj_fwd_1536x48x20480", "lib_us": round(lib_us, 1), "hip_us": round(hip_us, 1),
+                      "hip_GBps": round(nbytes / hip_us / 1e3, 1)}), flush=True)
+
+
 if __name__ == "__main__":
+    if "--small-k" in sys.argv:
+        small_k()
+        sys.exit(0)
     if "--epilogues" in sys.argv:
         load_gemm_tuning(model="vit_b16-mamba130m")
         epilogues()
