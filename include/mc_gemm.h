@@ -106,6 +106,15 @@ int mc_linear(const mc_linear_params* p, void* stream);
 int mc_gemm_small_k(int32_t M, int32_t K, int32_t T, int32_t dtype, const void* W, int64_t ldw, const void* X,
                     int64_t ldx, void* Y, int64_t ldy, void* stream);
 
+/*
+ * mc_gemm_skinny_m: Y (M x T) = W (M x K) X (K x T), 16-bit, fp32 accumulation summed in a fixed order,
+ * one rounding -- few output rows (M <= 96) over a long reduction (K % 256 == 0): the Mamba mixer's
+ * x_proj forward, x_dbl = W_x x (reference: Mamba's x_proj Linear; the SS2D form at model.py:519-528).
+ * Same layout requirements as mc_gemm_small_k.
+ */
+int mc_gemm_skinny_m(int32_t M, int32_t K, int32_t T, int32_t dtype, const void* W, int64_t ldw, const void* X,
+                     int64_t ldx, void* Y, int64_t ldy, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

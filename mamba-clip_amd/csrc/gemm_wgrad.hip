@@ -900,3 +900,162 @@ extern "C" int mc_gemm_small_k(int32_t M, int32_t K, int32_t T, int32_t dtype, c
   MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_small_k: launch failed: %s", hipGetErrorString(e));
   return MC_OK;
 }
+
+// ------------------------------------------------------------------ mc_gemm_skinny_m
+// Y (M x T) = W (M x K) X (K x T) for a few output rows (M <= 96) and a long reduction over X's rows
+// (K % 256 == 0): the Mamba mixer's x_proj forward, x_dbl = W_x x (80 x 1536 @ 1536 x B*L; reference:
+// Mamba's x_proj Linear, the SS2D form at model.py:519-528).  It is an HBM stream of X; the library
+// runs it at ~1/3 of that rate.  One workgroup = 64 tokens; its 4 waves split K four ways (each walks
+// its quarter in 64-row chunks: the next chunk's X rows and W fragments load into registers while the
+// current chunk's MFMAs run from the wave's own LDS image), then the four partial tiles are summed in a
+// fixed order ((w0 + w2) + (w1 + w3)) through the LDS and wave 0 writes Y in 128-B row pieces.
+namespace mc {
+namespace skinny {
+constexpr int kST = 64, kSC = 64, kSXRow = 160, kSORow = 144;   // tokens, K rows per chunk, LDS row bytes
+
+template <typename T, int MB>
+__global__ __launch_bounds__(256) void skinny_m_kernel(int M, int K, int Tn, const T* __restrict__ W, int64_t ldw,
+                                                       const T* __restrict__ X, int64_t ldx, T* __restrict__ Y,
+                                                       int64_t ldy) {
+  constexpr int kAcc = MB * 4;                          // f32x4 accumulators per lane
+  constexpr int kRed = 2 * kAcc * 4 * 64 * 4;           // two waves' partial tiles (bytes)
+  constexpr int kImg = 4 * kSC * kSXRow;                // the four waves' X images
+  constexpr int kOut = MB * 16 * kSORow;
+  constexpr int kLds = (kImg > kRed ? kImg : kRed) > kOut ? (kImg > kRed ? kImg : kRed) : kOut;
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int t0 = blockIdx.x * kST;
+  const int kq = K / 4, nchunk = kq / kSC, kw0 = w * kq;
+  char* img = lds + w * kSC * kSXRow;
+  // X chunk rows -> registers: vector v = lane + 64 j is row v / 8, tokens 8 (v % 8) .. + 7 (0 past Tn)
+  uint4 xr[8];
+  s16x4_t wn[MB][4];
+  auto load = [&](int c) __attribute__((always_inline)) {
+    const int k0 = kw0 + c * kSC;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int v = lane + 64 * j, r = v >> 3, col = (v & 7) * 8;
+      xr[j] = t0 + col < Tn ? ld16(X + (int64_t)(k0 + r) * ldx + t0 + col) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb) {
+      const int m = min(16 * cb + i, M - 1);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wn[cb][kk] = *reinterpret_cast<const s16x4_t*>(W + (int64_t)m * ldw + k0 + 16 * kk + 4 * g);
+    }
+  };
+  f32x4 acc[MB][4];
+#pragma unroll
+  for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb) acc[cb][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int c = 0; c < nchunk; ++c) {
+    // this wave's image only: a wave's LDS accesses complete in issue order, so no barrier
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int v = lane + 64 * j;
+      *reinterpret_cast<uint4*>(img + (v >> 3) * kSXRow + (v & 7) * 16) = xr[j];
+    }
+    s16x4_t wc[MB][4];
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wc[cb][kk] = wn[cb][kk];
+    if (c + 1 < nchunk) load(c + 1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) {
+        // B operand (k x t) by a transposed read: lane 4q + p addresses row 16 kk + 4 g + q, tokens 16 tb + 4 p
+        const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4_t*)((__attribute__((address_space(3))) char*)(img) + (16 * kk + 4 * g + q) * kSXRow + (16 * tb + 4 * p) * 2));
+#pragma unroll
+        for (int cb = 0; cb < MB; ++cb) acc[cb][tb] = mfma16<T>(wc[cb][kk], b, acc[cb][tb]);
+      }
+  }
+  // fixed-order sum of the four waves' partial tiles: (w0 + w2) + (w1 + w3)
+  float* red = reinterpret_cast<float*>(lds);
+  __syncthreads();
+  if (w >= 2) {
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(((w - 2) * kAcc + cb * 4 + tb) * 4 + j) * 64 + lane] = acc[cb][tb][j];
+  }
+  __syncthreads();
+  if (w < 2) {
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[cb][tb][j] += red[((w * kAcc + cb * 4 + tb) * 4 + j) * 64 + lane];
+  }
+  __syncthreads();
+  if (w == 1) {
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[((cb * 4 + tb) * 4 + j) * 64 + lane] = acc[cb][tb][j];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[cb][tb][j] += red[((cb * 4 + tb) * 4 + j) * 64 + lane];
+  }
+  __syncthreads();
+  if (w == 0) {
+    // C: lane holds rows 16 cb + 4 g + j of token 16 tb + i -> output image [rows][64 tokens] -> Y rows
+    T* out = reinterpret_cast<T*>(lds);
+#pragma unroll
+    for (int cb = 0; cb < MB; ++cb)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[(16 * cb + 4 * g + j) * (kSORow / 2) + 16 * tb + i] = from_f<T>(acc[cb][tb][j]);
+#pragma unroll
+    for (int j = 0; j < (MB * 16 * 8 + 63) / 64; ++j) {
+      const int v = lane + 64 * j, r = v >> 3, col = (v & 7) * 8;
+      if (r < MB * 16 && r < M && t0 + col < Tn)
+        st16(Y + (int64_t)r * ldy + t0 + col, *reinterpret_cast<const uint4*>(lds + r * kSORow + col * 2));
+    }
+  }
+}
+}  // namespace skinny
+}  // namespace mc
+
+extern "C" int mc_gemm_skinny_m(int32_t M, int32_t K, int32_t T, int32_t dtype, const void* W, int64_t ldw, const void* X,
+                                int64_t ldx, void* Y, int64_t ldy, void* stream) {
+  MC_CHECK(dtype == MC_DTYPE_BF16 || dtype == MC_DTYPE_F16, MC_ERR_DTYPE, "mc_gemm_skinny_m: bf16 / f16 only");
+  MC_CHECK(M > 0 && M <= 96 && K > 0 && K % 256 == 0 && T >= 0 && T % 8 == 0, MC_ERR_SHAPE,
+           "mc_gemm_skinny_m: 0 < M %d <= 96, K %d %% 256 == 0, T %d %% 8 == 0", M, K, T);
+  MC_CHECK(W && X && Y && aligned16(X) && aligned16(Y) && (reinterpret_cast<uintptr_t>(W) & 7) == 0 && ldw % 4 == 0 &&
+               ldw >= K && ldx % 8 == 0 && ldx >= T && ldy % 8 == 0 && ldy >= T,
+           MC_ERR_SHAPE, "mc_gemm_skinny_m: 16-B aligned X / Y rows (ld %% 8), 8-B aligned W rows");
+  MC_CHECK((int64_t)K * ldx < ((int64_t)1 << 40), MC_ERR_SHAPE, "mc_gemm_skinny_m: X too large");
+  if (T == 0) return MC_OK;
+  const dim3 grid((T + skinny::kST - 1) / skinny::kST), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  const int mb = (M + 15) / 16;
+#define MC_SKM(TT, MBV) hipLaunchKernelGGL((skinny::skinny_m_kernel<TT, MBV>), grid, block, 0, s, M, K, T, (const TT*)W, ldw, \
+                                           (const TT*)X, ldx, (TT*)Y, ldy)
+#define MC_SKM_T(TT) \
+  switch (mb) { case 1: MC_SKM(TT, 1); break; case 2: MC_SKM(TT, 2); break; case 3: MC_SKM(TT, 3); break; \
+                case 4: MC_SKM(TT, 4); break; case 5: MC_SKM(TT, 5); break; default: MC_SKM(TT, 6); break; }
+  if (dtype == MC_DTYPE_BF16) { MC_SKM_T(bf16_t) } else { MC_SKM_T(f16_t) }
+#undef MC_SKM_T
+#undef MC_SKM
+  hipError_t e = hipGetLastError();
+  MC_CHECK(e == hipSuccess, MC_ERR_LAUNCH, "mc_gemm_skinny_m: launch failed: %s", hipGetErrorString(e));
+  return MC_OK;
+}

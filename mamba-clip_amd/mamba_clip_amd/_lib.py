@@ -248,6 +248,7 @@ SYMBOLS = {
     "mc_linear_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(LinearParams)]),
     "mc_linear": (ctypes.c_int, [ctypes.POINTER(LinearParams), c_vp]),
     "mc_gemm_small_k": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mc_gemm_skinny_m": (ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mc_scan_bwd_kernel": (c_i32, [ctypes.POINTER(ScanBwdParams)]),
     "mc_scan_chunk_states_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
     "mc_scan_fwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),

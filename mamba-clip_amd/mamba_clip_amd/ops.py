@@ -1157,6 +1157,31 @@ def gemm_small_k(wc, Xc):
     return y
 
 
+# w @ X with few output rows and a long reduction (the mixer's x_proj forward, 80 x 1536) on
+# mc_gemm_skinny_m.  A/B toggle, off: as built it streams X at 1.7 TB/s (38.3 vs the library's 25.7 us at
+# C2; step +0.1-0.25 ms, profiles/r05/mixer/) -- one 8 KB chunk in flight per wave, latency-bound.
+SKINNY_M_HIP = os.environ.get("MAMBA_CLIP_AMD_SKINNY_M_HIP", "0") == "1"
+
+
+def skinny_m_ok(wc, Xc):
+    M, K = wc.shape
+    return (SKINNY_M_HIP and Xc.is_cuda and wc.dtype == Xc.dtype and Xc.dtype in (torch.bfloat16, torch.float16)
+            and 0 < M <= 96 and K % 256 == 0 and Xc.shape[1] % 8 == 0 and Xc.stride(1) == 1
+            and Xc.stride(0) % 8 == 0 and Xc.data_ptr() % 16 == 0 and wc.stride(1) == 1 and wc.stride(0) % 4 == 0
+            and wc.data_ptr() % 8 == 0)
+
+
+def gemm_skinny_m(wc, Xc):
+    """wc (M, K) @ Xc (K, T) on mc_gemm_skinny_m (caller checks skinny_m_ok)."""
+    M, K = wc.shape
+    T = Xc.shape[1]
+    y = torch.empty(M, T, device=Xc.device, dtype=Xc.dtype)
+    _lib.check(_lib.load().mc_gemm_skinny_m(M, K, T, _lib.dtype_code(Xc.dtype), wc.data_ptr(), wc.stride(0),
+                                            Xc.data_ptr(), Xc.stride(0), y.data_ptr(), T,
+                                            _lib.stream_handle(Xc.device)), "mc_gemm_skinny_m")
+    return y
+
+
 class WeightLeftMM(torch.autograd.Function):
     """y = w @ X for a weight w (N, K) and activations X (K, M) (channel-major GEMMs of the Mamba mixer)."""
 
@@ -1165,7 +1190,12 @@ class WeightLeftMM(torch.autograd.Function):
         dt = _compute_dtype(X)
         wc, Xc = _wcast(weight, dt), X.to(dt)
         with torch.autocast("cuda", enabled=False):
-            y = gemm_small_k(wc, Xc) if small_k_ok(wc, Xc) else torch.mm(wc, Xc)
+            if small_k_ok(wc, Xc):
+                y = gemm_small_k(wc, Xc)
+            elif skinny_m_ok(wc, Xc):
+                y = gemm_skinny_m(wc, Xc)
+            else:
+                y = torch.mm(wc, Xc)
         ctx.save_for_backward(wc, Xc)
         ctx.handoff = handoff
         ctx.out_slab = out_slab   # (GradSlab, first row): dX written into those rows (ops.GradSlab)

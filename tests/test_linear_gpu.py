@@ -190,3 +190,23 @@ def test_gemm_small_k(M, K, T, dt):
     err = (y.double() - ref).abs()
     assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
     assert torch.equal(y, ops.gemm_small_k(w, x))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K,T", [(80, 1536, 20480), (80, 1536, 640), (96, 3072, 2056), (20, 256, 8), (17, 512, 136)])
+def test_gemm_skinny_m(M, K, T, dt, monkeypatch):
+    """mc_gemm_skinny_m (the mixer's x_proj forward; off by default) vs an fp64 product of the same
+    operands; X a row view of a wider buffer, ragged M and T; bitwise repeatable (fixed-order sum of the
+    waves' K quarters)."""
+    monkeypatch.setattr(ops, "SKINNY_M_HIP", True)
+    g = torch.Generator(device=DEV).manual_seed(M + K + T)
+    w = _rand((M, K), dt, g, 0.05)
+    xb = _rand((K, T + 24), dt, g)
+    x = xb[:, :T]                                              # row stride T + 24
+    assert ops.skinny_m_ok(w, x)
+    y = ops.gemm_skinny_m(w, x)
+    ref = w.double() @ x.double()
+    bound = (w.double().abs() @ x.double().abs()) * 1e-5 + ref.abs() * ULP[dt] / 2 + 1e-6
+    err = (y.double() - ref).abs()
+    assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
+    assert torch.equal(y, ops.gemm_skinny_m(w, x))

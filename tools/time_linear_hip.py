@@ -115,6 +115,12 @@ def small_k():
     nbytes = 1536 * 20480 * 2 + 48 * 20480 * 2
     print(json.dumps({"case": "dt_proj_fwd_1536x48x20480", "lib_us": round(lib_us, 1), "hip_us": round(hip_us, 1),
                       "hip_GBps": round(nbytes / hip_us / 1e3, 1)}), flush=True)
+    wx = ((torch.rand(80, 1536, device=DEV, generator=g) * 2 - 1) * 0.05).to(bf)
+    xc = (torch.rand(1536, 20480, device=DEV, generator=g) * 2 - 1).to(bf)
+    lib_us, hip_us = timed(lambda: torch.mm(wx, xc)), timed(lambda: ops.gemm_skinny_m(wx, xc))
+    nbytes = 1536 * 20480 * 2 + 80 * 20480 * 2
+    print(json.dumps({"case": "x_proj_fwd_80x1536x20480", "lib_us": round(lib_us, 1), "hip_us": round(hip_us, 1),
+                      "hip_GBps": round(nbytes / hip_us / 1e3, 1)}), flush=True)
 
 
 if __name__ == "__main__":
