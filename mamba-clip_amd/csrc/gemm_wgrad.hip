@@ -710,17 +710,24 @@ extern "C" int mc_gemm_wgrad(const mc_wgrad_params* p, void* stream) {
 // Y = X W^T on wgrad4p_kernel with both operands feature-major in its terms (A = W: row m = output
 // feature, B = X: row n = token, unit stride along K) and a 16-bit epilogue; one workgroup per
 // 256 x 256 output tile (K <= a few thousand: no split).
-template <typename T>
-static void launch_linear(const Args& a, int epi, hipStream_t s) {
+template <typename T, bool kStag>
+static void launch_linear_s(const Args& a, int epi, hipStream_t s) {
   const dim3 grid(a.tiles_m * a.tiles_n), block(kThreads);
   switch (epi) {
-    case MC_LINEAR_EPI_NONE: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiStore>), grid, block, 0, s, a); break;
-    case MC_LINEAR_EPI_BIAS: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiBias>), grid, block, 0, s, a); break;
+    case MC_LINEAR_EPI_NONE: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, kStag, kEpiStore>), grid, block, 0, s, a); break;
+    case MC_LINEAR_EPI_BIAS: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, kStag, kEpiBias>), grid, block, 0, s, a); break;
     case MC_LINEAR_EPI_BIAS_GELU:
-      hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiBiasGelu>), grid, block, 0, s, a);
+      hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, kStag, kEpiBiasGelu>), grid, block, 0, s, a);
       break;
-    default: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, true, kEpiGeluGrad>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((wgrad4p_kernel<T, true, true, kStag, kEpiGeluGrad>), grid, block, 0, s, a); break;
   }
+}
+// MC_LINEAR_STAGGER=0: wave rows in step (A/B of the staggered schedule at these short K loops)
+template <typename T>
+static void launch_linear(const Args& a, int epi, hipStream_t s) {
+  const char* e = getenv("MC_LINEAR_STAGGER");
+  if (e && atoi(e) == 0) launch_linear_s<T, false>(a, epi, s);
+  else launch_linear_s<T, true>(a, epi, s);
 }
 
 static int linear_check(const mc_linear_params* p) {

@@ -100,7 +100,11 @@ def epilogues():
     ]
     for name, flop, lib_fn, hip_fn in cases:
         lib_us, hip_us = timed(lib_fn), timed(hip_fn)
+        os.environ["MC_LINEAR_STAGGER"] = "0"
+        hip_us_nostag = timed(hip_fn)
+        os.environ.pop("MC_LINEAR_STAGGER")
         print(json.dumps({"case": name, "lib_chain_us": round(lib_us, 1), "hip_us": round(hip_us, 1),
+                          "hip_us_rows_in_step": round(hip_us_nostag, 1),
                           "hip_gemm_tflops": round(flop / hip_us / 1e6, 1)}), flush=True)
 
 
