@@ -296,9 +296,11 @@ __device__ __forceinline__ void half_sources(const char* base, int64_t ld, int d
 // (lgkmcnt(0)) BEFORE its first barrier: the half-tile restaged one phase later is only written after
 // that barrier, which both rows have passed with their reads of it done (cdna_hip_programming.md
 // section 5: "one barrier MORE when two wave groups run staggered").
+constexpr int kHPre = 8;   // kEpiGeluGrad: H vectors per thread requested during the last K step
+
 template <typename T, int kEpi>
 __device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4 (&acc)[2][2][4][2], int m0, int n0,
-                                           int tn, int wr, int wc, int fg, int fi, int tid);
+                                           int tn, int wr, int wc, int fg, int fi, int tid, const uint4 (&hpre)[kHPre]);
 
 template <typename T, bool kAFM, bool kBFM, bool kStagger, int kEpi = kEpiSlab>
 __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
@@ -431,8 +433,21 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
 
   s16x8 af[4][2], bf0[2][2], bf1[2][2];
   if (kStagger && wr == 1) __builtin_amdgcn_s_barrier();   // wr is wave-uniform (readfirstlane'd w)
+  // kEpiGeluGrad: the epilogue's first H vectors are requested at the start of the last K step, so their
+  // latency hides behind its MFMAs (nothing else is in flight then: the step before retired with vmcnt(0))
+  uint4 hpre[kHPre];
   for (int t = 0; t < nk; ++t) {
     const char* st = lds + (t & 1) * 4 * kHalf;
+    if constexpr (kEpi == kEpiGeluGrad) {
+      if (t == nk - 1) {
+        const int c = tid & 31, sub = tid >> 5, f = m0 + c * 8;
+#pragma unroll
+        for (int p = 0; p < kHPre; ++p) {
+          const int tt = min(n0 + p * 16 + sub, g.N - 1);
+          hpre[p] = f < g.M ? ld16(reinterpret_cast<const T*>(g.H) + (int64_t)tt * g.ldh + f) : make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
     // ---- phase 1: B qn0 + A qm0 -> quadrant (0, 0); stage B h0 of step t + 1
     read_b(st + 2 * kHalf, bf0);
     read_a(st + 0 * kHalf, af);
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
   if (kStagger && wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both rows
 
   if constexpr (kEpi != kEpiSlab) {
-    epilogue16<T, kEpi>(g, lds, acc, m0, n0, tn, wr, wc, fg, fi, tid);
+    epilogue16<T, kEpi>(g, lds, acc, m0, n0, tn, wr, wc, fg, fi, tid, hpre);
     return;
   }
   // ---- epilogue: quadrant (qm, qn), tile (mi, ni): rows wr*128 + qm*64 + mi*16 + 4 (l >> 4) + r,
@@ -500,7 +515,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad4p_kernel(const Args g) {
 // LDS in a fixed order: one fp32 partial per (token tile, feature), folded by the caller.
 template <typename T, int kEpi>
 __device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4 (&acc)[2][2][4][2], int m0, int n0,
-                                           int tn, int wr, int wc, int fg, int fi, int tid) {
+                                           int tn, int wr, int wc, int fg, int fi, int tid, const uint4 (&hpre)[kHPre]) {
   const int c = tid & 31, sub = tid >> 5;   // read-back: chunk of 8 features, row within a group of 16
   const int f = m0 + c * 8;
   const bool fok = f < g.M;
@@ -511,7 +526,8 @@ __device__ __forceinline__ void epilogue16(const Args& g, char* lds, const f32x4
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
       const int t = min(n0 + p * 16 + sub, g.N - 1);
-      hq[p] = fok ? ld16(reinterpret_cast<const T*>(g.H) + (int64_t)t * g.ldh + f) : make_uint4(0, 0, 0, 0);
+      hq[p] = p < kHPre ? hpre[p]
+                        : (fok ? ld16(reinterpret_cast<const T*>(g.H) + (int64_t)t * g.ldh + f) : make_uint4(0, 0, 0, 0));
     }
   }
 #pragma unroll
