@@ -88,7 +88,7 @@ __device__ __forceinline__ float halve_bit3(float a, float b) {
   float r;
   asm volatile("s_nop 1\n\t"
                "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
-               "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+               "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc" MC_ASM_TAIL
                : "=&v"(r) : "v"(a), "v"(b));
   return r;
 }
@@ -96,7 +96,7 @@ __device__ __forceinline__ float halve_bit2(float a, float b) {
   float r;
   asm volatile("s_nop 1\n\t"
                "v_add_f32_dpp %0, %1, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
-               "v_add_f32_dpp %0, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa"
+               "v_add_f32_dpp %0, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa" MC_ASM_TAIL
                : "=&v"(r) : "v"(a), "v"(b));
   return r;
 }
@@ -108,11 +108,11 @@ __device__ __forceinline__ float halve_bit2(float a, float b) {
 // of 4 selects, 2 adds, a DPP move and an add.  Same sums, same order as before.
 __device__ __forceinline__ float pair_finish(f32x2 a, f32x2 b, int h) {
   float sa, sb, r;
-  asm("v_add_f32_e32 %0, %1, %2" : "=v"(sa) : "v"(a.x), "v"(a.y));
-  asm("v_add_f32_e32 %0, %1, %2" : "=v"(sb) : "v"(b.x), "v"(b.y));
+  asm("v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sa) : "v"(a.x), "v"(a.y));
+  asm("v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sb) : "v"(b.x), "v"(b.y));
   const float keep = h ? sb : sa, send = h ? sa : sb;
   asm("s_nop 1\n\t"
-      "v_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      "v_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" MC_ASM_TAIL
       : "=v"(r) : "v"(send), "v"(keep));
   return r;
 }
@@ -123,6 +123,12 @@ __device__ __forceinline__ float pair_finish(f32x2 a, f32x2 b, int h) {
 // then a full add over bit 1.  (An LDS transpose -- 16 b32 writes, 4 b128 reads, 8 packed adds --
 // cut the VALU count by a fifth but measured 9 % slower: the round trip sits on each pair's path.)
 __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
+  // gfx950: v_permlane*_swap must not read a VGPR within 2 wait states of the VALU op that wrote it.  The
+  // compiler pads its own producers (s_nop 1) but gives an inline-asm producer only 1 wait state, and
+  // v[] comes from pk_mul_bcast (asm).  Routing the operands through an s_nop 1 that "defines" them puts
+  // >= 2 wait states between the last product and the first swap (tools/hazard_scan.py).
+  asm volatile("s_nop 1" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+               "+v"(v[7]));
 #pragma unroll
   for (int t = 0; t < 4; ++t) {   // bit 5: t <-> t + 4
     const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 4].x), false, false);

@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Localise the two-stream C2 step's run-to-run divergence.
+
+Runs the C2 forward + ClipLoss + backward (towers on two streams, default hardware queues) --runs times
+from the same parameters.  The first scan backward of the step (text layer 23) is wrapped: right AFTER
+the real call (so the kernel itself runs in the step's normal concurrency) every input and output is
+cloned on the same stream.  After the step the device is synchronised and the same backward is re-run
+twice on the cloned inputs on a quiet device ("solo").  Per run it reports, bitwise:
+  - which outputs differ between the in-step call and the solo re-run (inputs identical by construction),
+  - which inputs / outputs differ from run 0,
+  - for ddelta elements that differ in-step vs solo: where they sit in the pair kernel's decomposition
+    (workgroup block of 128 channels, wave, chunk of 32 positions, 8-position sub-tile, lane half) and
+    the batch index,
+  - the layer-23 dt_proj / D / A_log gradients vs run 0.
+  python3 tools/scan_bwd_localize.py --batch 32 --runs 6
+"""
+import argparse
+import collections
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+import torch  # noqa: E402
+
+OUT_NAMES = ("du", "ddelta", "dA", "dB", "dC", "dD", "dz", "dbias")
+IN_NAMES = ("u", "delta", "A", "B", "C", "D", "z", "delta_bias", "softplus", "dout", "states")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--runs", type=int, default=6)
+    ap.add_argument("--call", type=int, default=0, help="which scan backward of the step to wrap (0 = layer 23)")
+    ap.add_argument("--concurrent", type=int, default=1)
+    ap.add_argument("--pre-clone", action="store_true", help="also clone the inputs right BEFORE the call")
+    args = ap.parse_args()
+
+    from mamba_clip_amd import selective_scan_interface as ssi
+    from mamba_clip_amd.data import synthetic_batch
+    from mamba_clip_amd.loss import ClipLoss
+    from mamba_clip_amd.model import build_clip
+    from mamba_clip_amd.tuning import load_gemm_tuning
+
+    dev = torch.device("cuda", 0)
+    load_gemm_tuning(model="vit_b16-mamba130m")
+    torch.manual_seed(0)
+    model = build_clip("vit_b16-mamba130m").to(dev)
+    model.concurrent_towers = bool(args.concurrent)
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    images, texts, _ = synthetic_batch(args.batch, 224, model.text.context_length, model.text.vocab_size,
+                                       device=dev, seed=1000)
+    loss_fn = ClipLoss()
+    real_bwd = ssi.scan_bwd
+    state = {"n": 0, "rec": None}
+
+    def cl(x):
+        return x.detach().clone() if isinstance(x, torch.Tensor) else x
+
+    def wrapped(*a, **k):
+        i = state["n"]
+        state["n"] += 1
+        if i != args.call:
+            return real_bwd(*a, **k)
+        pre = tuple(cl(x) for x in a) if args.pre_clone else None
+        out = real_bwd(*a, **k)
+        state["rec"] = {"ins": tuple(cl(x) for x in a), "outs": tuple(cl(x) for x in out), "pre": pre,
+                        "stream": torch.cuda.current_stream().cuda_stream}
+        return out
+
+    ssi.scan_bwd = wrapped
+    L23 = model.text.layers[-1].mixer
+    runs = []
+    for r in range(args.runs):
+        model.load_state_dict(init)
+        model.zero_grad(set_to_none=True)
+        state["n"], state["rec"] = 0, None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(images, texts)
+            loss = loss_fn(**out)["contrastive_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+        rec = state["rec"]
+        ins = rec["ins"]
+        solo = [real_bwd(*ins) for _ in range(2)]
+        torch.cuda.synchronize()
+        rec["solo"] = [tuple(cl(x) for x in s) for s in solo]
+        rec["grads"] = {"dt_proj.bias": L23.dt_proj.bias.grad.clone(), "dt_proj.weight": L23.dt_proj.weight.grad.clone(),
+                        "D": L23.D.grad.clone(), "A_log": L23.A_log.grad.clone(),
+                        "x_proj.weight": L23.x_proj.weight.grad.clone(), "out_proj.weight": L23.out_proj.weight.grad.clone()}
+        rec["loss"] = float(loss)
+        runs.append(rec)
+        line = {"run": r, "loss": rec["loss"], "n_scan_bwd": state["n"]}
+
+        def eqt(x, y):
+            if isinstance(x, torch.Tensor):
+                return bool(isinstance(y, torch.Tensor) and x.shape == y.shape and torch.equal(x, y))
+            return x == y
+        line["solo_repeat_equal"] = all(eqt(x, y) for x, y in zip(rec["solo"][0], rec["solo"][1]))
+        line["instep_vs_solo_differ"] = {}
+        for j, nm in enumerate(OUT_NAMES):
+            x, y = rec["outs"][j], rec["solo"][0][j]
+            if isinstance(x, torch.Tensor) and not eqt(x, y):
+                line["instep_vs_solo_differ"][nm] = {"n": int((x != y).sum()), "numel": x.numel(),
+                                                     "max_abs": float((x.float() - y.float()).abs().max())}
+        if args.pre_clone:
+            line["inputs_changed_during_call"] = [IN_NAMES[j] for j, (x, y) in enumerate(zip(rec["pre"], ins))
+                                                  if isinstance(x, torch.Tensor) and not eqt(x, y)]
+        dd_x, dd_y = rec["outs"][1], rec["solo"][0][1]
+        if not eqt(dd_x, dd_y):
+            idx = (dd_x != dd_y).nonzero()
+            b, d, l = idx[:, 0], idx[:, 1], idx[:, 2]
+            cnt = lambda t: dict(sorted(collections.Counter(t.tolist()).items())[:40])
+            line["ddelta_diff_where"] = {"batch": cnt(b), "wblk": cnt(d // 128), "wave": cnt((d % 128) // 32),
+                                         "chunk": cnt(l // 32), "subtile": cnt((l % 32) // 8), "half": cnt((l % 8) // 4),
+                                         "channel_in_wave": cnt(d % 32), "first": idx[:8].tolist()}
+        if r > 0:
+            r0 = runs[0]
+            line["inputs_vs_run0_differ"] = [IN_NAMES[j] for j, (x, y) in enumerate(zip(r0["ins"], ins))
+                                             if isinstance(x, torch.Tensor) and not eqt(x, y)]
+            line["instep_outs_vs_run0_differ"] = [OUT_NAMES[j] for j, (x, y) in enumerate(zip(r0["outs"], rec["outs"]))
+                                                  if isinstance(x, torch.Tensor) and not eqt(x, y)]
+            line["solo_outs_vs_run0_solo_differ"] = [OUT_NAMES[j] for j, (x, y) in
+                                                     enumerate(zip(r0["solo"][0], rec["solo"][0]))
+                                                     if isinstance(x, torch.Tensor) and not eqt(x, y)]
+            line["layer23_grads_vs_run0_differ"] = [k for k in rec["grads"] if not eqt(r0["grads"][k], rec["grads"][k])]
+            line["loss_equal_run0"] = rec["loss"] == r0["loss"]
+        # keep memory bounded: only run 0's record and the current one
+        if r > 0:
+            runs[-1] = {k: v for k, v in rec.items() if k in ()}
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
