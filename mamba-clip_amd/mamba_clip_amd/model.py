@@ -37,6 +37,7 @@ from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_pos,
                   packed_attention, patch_im2col, qkv_proj, split_rows, split_rows_n, ss2d_conv_stack,
                   ss2d_merge_ln_gate, token_embed, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
+                                       fine_state_scope,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
 
 
@@ -206,11 +207,18 @@ class MambaTextEncoder(nn.Module):
         As = (neg_exp_many([l.mixer.A_log for l in self.layers]) if hidden.is_cuda
               else [None] * len(self.layers))
         ckpt = self.grad_checkpointing and torch.is_grad_enabled()
+        n = len(self.layers)
+
+        def run(layer, hidden, residual, A):
+            # each layer's scan may keep fine saved states within budget / n_layer (a static choice: the
+            # same in the checkpoint recompute, which runs on the autograd thread)
+            with fine_state_scope(n):
+                return layer(hidden, residual, A)
         for layer, A in zip(self.layers, As):
             if ckpt:   # recompute the layer in backward instead of keeping its activations
-                hidden, residual = torch.utils.checkpoint.checkpoint(layer, hidden, residual, A, use_reentrant=False)
+                hidden, residual = torch.utils.checkpoint.checkpoint(run, layer, hidden, residual, A, use_reentrant=False)
             else:
-                hidden, residual = layer(hidden, residual, A)
+                hidden, residual = run(layer, hidden, residual, A)
         normed, _ = add_rmsnorm(hidden, residual, self.norm_f)
         pooled = normed[:, T - 1]                                   # EOT position
         return self.proj(pooled)

@@ -785,9 +785,14 @@ class L2NormalizeFn(torch.autograd.Function):
 
 
 def l2_normalize(x, eps=1e-12):
-    """F.normalize(x, dim=-1) on the GPU kernels for 2-D CUDA tensors (fp32 result); torch elsewhere."""
+    """F.normalize(x, dim=-1) on the GPU kernels for 2-D CUDA tensors; torch elsewhere.  Result dtype as
+    torch's: fp32 under CUDA autocast (norm runs in fp32 there and the division promotes), the input's
+    dtype otherwise (pure_bf16 / pure_fp16 precisions)."""
     if x.is_cuda and x.dim() == 2 and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and x.shape[1] > 0:
-        return L2NormalizeFn.apply(x, eps)
+        y = L2NormalizeFn.apply(x, eps)
+        if x.dtype != torch.float32 and not torch.is_autocast_enabled("cuda"):
+            y = y.to(x.dtype)
+        return y
     return torch.nn.functional.normalize(x, dim=-1, eps=eps)
 
 
@@ -1429,12 +1434,15 @@ class MlpFn(torch.autograd.Function):
         w1c, b1c, w2c, b2c = _wcast(w1, dt), _wcast(b1, dt), _wcast(w2, dt), _wcast(b2, dt)
         x2 = xc.reshape(-1, xc.shape[-1])
         with torch.autocast("cuda", enabled=False):
-            if MLP_HIP_FC1:
+            # each mc_linear call is guarded by linear_hip_ok (strides / 16-B alignment the kernel needs);
+            # an ineligible operand takes the library GEMM instead of failing the step
+            if MLP_HIP_FC1 and linear_hip_ok(x2, w1c):
                 h, a = linear_hip(x2, w1c, b1c, _lib.MC_LINEAR_EPI_BIAS_GELU)
             else:
                 h = torch.nn.functional.linear(x2, w1c, b1c)
                 a = torch.nn.functional.gelu(h)
-            y = linear_hip(a, w2c, b2c) if MLP_HIP_FC2 else torch.nn.functional.linear(a, w2c, b2c)
+            y = (linear_hip(a, w2c, b2c) if MLP_HIP_FC2 and linear_hip_ok(a, w2c)
+                 else torch.nn.functional.linear(a, w2c, b2c))
         ctx.save_for_backward(x2, h, a, w1c, w2c)
         ctx.wt1, ctx.wt2 = _wcast_t(w1, xc, dt), _wcast_t(w2, a, dt)
         ctx.xshape = xc.shape
@@ -1452,16 +1460,16 @@ class MlpFn(torch.autograd.Function):
         else:
             db2 = colsum(g2)
         dw2 = wgrad(g2.t(), a)
-        if MLP_HIP_BWD:
-            wt2 = ctx.wt2 if ctx.wt2 is not None else w2c.t().contiguous()
+        wt2 = (ctx.wt2 if ctx.wt2 is not None else w2c.t().contiguous()) if MLP_HIP_BWD else None
+        if MLP_HIP_BWD and linear_hip_ok(g2, wt2) and _aligned_rows(h, 8):
             gh, db1 = linear_hip(g2, wt2, None, _lib.MC_LINEAR_EPI_GELU_GRAD, h=h, want_colsum=True)
         else:
             gh, db1 = _gelu_bwd(h, _dgrad(g2, w2c, ctx.wt2))
         dw1 = wgrad(gh.t(), x2)
         dx = None
         if ctx.needs_input_grad[0]:
-            if MLP_HIP_BWD:
-                wt1 = ctx.wt1 if ctx.wt1 is not None else w1c.t().contiguous()
+            wt1 = (ctx.wt1 if ctx.wt1 is not None else w1c.t().contiguous()) if MLP_HIP_BWD else None
+            if MLP_HIP_BWD and linear_hip_ok(gh, wt1):
                 dx = linear_hip(gh, wt1)
             else:
                 dx = _dgrad(gh, w1c, ctx.wt1)

@@ -11,8 +11,9 @@ fp32 chunk states (one per MC_SCAN_CHUNK positions); the backward runs
 ``mc_scan_bwd`` from them.  Both launch on the current HIP stream and never
 synchronise.  There is no CPU / eager fallback.
 """
+import contextlib
 import os
-import weakref
+import threading
 
 import torch
 
@@ -60,25 +61,37 @@ def _check_inputs(u, delta, A, B, C, D, z, delta_bias):
 
 
 def fine_states_max_bytes():
-    """Budget (bytes) for the fine saved states alive at once, over every scan call of the process (a
-    whole training step's layers, not one call).  The fine interval costs 4x the default interval's
-    memory and buys the backward's recompute pass: a C2 layer holds 252 MB of fine states instead of
-    63 MB, 6.0 GB instead of 1.5 GB for the 24 layers; a C4 layer (L 4096) would need 6.4 GB.  Calls
-    that would take the live total past the budget save the default interval instead (later layers of
-    a larger batch degrade gracefully rather than run out of memory).  MAMBA_CLIP_AMD_FINE_STATES_MB
-    sets it (default 8192 MB = C2 at batch 256 plus margin; 0 = never)."""
+    """Budget (bytes) for the fine saved states of one step's scan calls.  The fine interval costs 4x
+    the default interval's memory and buys the backward's recompute pass: a C2 layer holds 252 MB of
+    fine states instead of 63 MB, 6.0 GB instead of 1.5 GB for the 24 layers; a C4 layer (L 4096) would
+    need 6.4 GB.  MAMBA_CLIP_AMD_FINE_STATES_MB sets it (default 8192 MB = C2 at batch 256 plus margin;
+    0 = never)."""
     return int(float(os.environ.get("MAMBA_CLIP_AMD_FINE_STATES_MB", "8192")) * (1 << 20))
 
 
-_FINE_LIVE = [0]   # bytes of fine saved states currently alive (released when the tensor is freed)
+_FINE_SCOPE = threading.local()   # .calls: scan calls per step declared by the innermost fine_state_scope
 
 
-def _fine_release(nbytes):
-    _FINE_LIVE[0] -= nbytes
+@contextlib.contextmanager
+def fine_state_scope(n_calls):
+    """Declare that the enclosed forward makes ``n_calls`` training scan calls (a tower's layer count):
+    each call may then take the fine interval when its own fine states fit ``budget / n_calls``.
+
+    The choice is a function of the call's shapes, the budget and the declared count only -- never of
+    what other autograd graphs happen to be alive (round 5 counted live bytes released by finalizers,
+    so eval passes, checkpoint recompute or graph warm-up changed which interval, hence which bits, a
+    layer produced: ADVICE r05).  Outside any scope a call counts as the step's only one."""
+    prev = getattr(_FINE_SCOPE, "calls", None)
+    _FINE_SCOPE.calls = max(1, int(n_calls))
+    try:
+        yield
+    finally:
+        _FINE_SCOPE.calls = prev
 
 
-def fine_states_live_bytes():
-    return _FINE_LIVE[0]
+def fine_states_allowance():
+    """Bytes of fine saved states one scan call may take (budget / declared calls per step)."""
+    return fine_states_max_bytes() // (getattr(_FINE_SCOPE, "calls", None) or 1)
 
 
 def states_interval(L, dim, states):
@@ -154,15 +167,12 @@ def scan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus, want_states, w
         # the backward then reads each sub-tile's entry state instead of recomputing it
         fine = _lib.MC_SCAN_STATE_INTERVAL_FINE
         fine_bytes = batch * dim * lib.mc_scan_n_states(L, fine) * dstate * 4
-        if _FINE_LIVE[0] + fine_bytes <= fine_states_max_bytes():
+        if fine_bytes <= fine_states_allowance():
             p.state_interval = fine
             p.state_interval = lib.mc_scan_fwd_state_interval(p)
         nch = lib.mc_scan_n_states(L, p.state_interval)
         shape = (batch, nch, dim, dstate) if p.state_interval == fine else (batch, dim, nch, dstate)
         states = torch.empty(shape, device=u.device, dtype=torch.float32)
-        if p.state_interval == fine:
-            _FINE_LIVE[0] += fine_bytes
-            weakref.finalize(states, _fine_release, fine_bytes)
         p.chunk_states = states.data_ptr()
     if RECORD_DISPATCH:
         DISPATCH.append(("fwd", int(lib.mc_scan_fwd_kernel(p))))

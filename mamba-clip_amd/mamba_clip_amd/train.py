@@ -268,6 +268,12 @@ class GraphedStep:
             # the mixup draws lam (and the lam > 0.5 text swap) on the host: a replay would repeat the
             # capture's draw forever
             raise ValueError("GraphedStep: balanced_mixup draws host-side randomness per step; run it eager")
+        if concurrent and os.environ.get("GPU_MAX_HW_QUEUES", "").strip() == "1":
+            # Capturing the towers' fork / join with both streams on one hardware queue ended the process
+            # with SIGSEGV inside the HIP runtime's capture path (round 5); one hardware queue
+            # serialises the two streams anyway, so the one-stream capture loses nothing there.
+            raise ValueError("GraphedStep(concurrent=True) is not supported with GPU_MAX_HW_QUEUES=1 "
+                             "(the two streams share one hardware queue): use concurrent=False")
         autocast = self.autocast_for(args)
         inner = unwrap_model(model)
         # One stream by default: replay order = eager order, and the replays are bitwise repeatable.
