@@ -84,6 +84,7 @@ __device__ __forceinline__ float row_xor4(float v) {   // banks 0 / 2 take lane 
 // b + b[lane ^ 8]; halve_bit2: bit 2 clear -> a + a[lane + 4], set -> b + b[lane - 4].  The leading
 // s_nop 1 covers the VALU-write -> DPP-read hazard (hipcc pads nothing inside asm).  Same sums,
 // same order as the select form (own + partner).
+#ifndef MC_BWD_SELECT_HALVES
 __device__ __forceinline__ float halve_bit3(float a, float b) {
   float r;
   asm volatile("s_nop 1\n\t"
@@ -100,22 +101,43 @@ __device__ __forceinline__ float halve_bit2(float a, float b) {
                : "=&v"(r) : "v"(a), "v"(b));
   return r;
 }
+#else
+// A/B (hazard audit): the same halvings as keep / send selects around compiler DPP moves
+__device__ __forceinline__ float halve_bit3(float a, float b) {
+  const bool hi = (__lane_id() >> 3) & 1;
+  const float keep = hi ? b : a, send = hi ? a : b;
+  return keep + row_xor8(send);
+}
+__device__ __forceinline__ float halve_bit2(float a, float b) {
+  const bool hi = (__lane_id() >> 2) & 1;
+  const float keep = hi ? b : a, send = hi ? a : b;
+  return keep + row_xor4(send);
+}
+#endif
 
 // Finishing of one position's state sums: lanes of half h keep pair (h ? b : a) and add the partner
 // lane's (lane ^ 1) other pair, each pair summed over its two states first.  The two pair sums and
 // the DPP add are asm so that the compiler neither SLP-packs the sums (it did, into more
 // instructions) nor keeps the DPP move apart from the add: 2 adds, 2 selects, 1 DPP add instead
 // of 4 selects, 2 adds, a DPP move and an add.  Same sums, same order as before.
+#ifndef MC_BWD_C_FINISH
 __device__ __forceinline__ float pair_finish(f32x2 a, f32x2 b, int h) {
   float sa, sb, r;
-  asm("v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sa) : "v"(a.x), "v"(a.y));
-  asm("v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sb) : "v"(b.x), "v"(b.y));
+  asm(MC_ASM_HEAD "v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sa) : "v"(a.x), "v"(a.y));
+  asm(MC_ASM_HEAD "v_add_f32_e32 %0, %1, %2" MC_ASM_TAIL : "=v"(sb) : "v"(b.x), "v"(b.y));
   const float keep = h ? sb : sa, send = h ? sa : sb;
   asm("s_nop 1\n\t"
       "v_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" MC_ASM_TAIL
       : "=v"(r) : "v"(send), "v"(keep));
   return r;
 }
+#else
+__device__ __forceinline__ float pair_finish(f32x2 a, f32x2 b, int h) {   // A/B (hazard audit): compiler code
+  const float sa = a.x + a.y, sb = b.x + b.y;
+  const float keep = h ? sb : sa, send = h ? sa : sb;
+  return keep + qperm<kQpXor1>(send);
+}
+#endif
 
 // Sum of 16 per-lane values (8 packed pairs, value k = 2t + s in v[t].{x|y}) over the 32 lanes of
 // the same lane bit 0 (the wave's 32 channels).  Lane l ends with value k = l >> 2 (lanes l and l ^ 2
@@ -131,14 +153,20 @@ __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
                "+v"(v[7]));
 #pragma unroll
   for (int t = 0; t < 4; ++t) {   // bit 5: t <-> t + 4
-    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 4].x), false, false);
-    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].y), __float_as_uint(v[t + 4].y), false, false);
+    auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 4].x), false, false);
+    auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].y), __float_as_uint(v[t + 4].y), false, false);
+#ifdef MC_PERMLANE_NOP
+    asm volatile("s_nop 4" : "+v"(rx[0]), "+v"(rx[1]), "+v"(ry[0]), "+v"(ry[1]));
+#endif
     v[t] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {   // bit 4: t <-> t + 2
-    const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 2].x), false, false);
-    const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[t].y), __float_as_uint(v[t + 2].y), false, false);
+    auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 2].x), false, false);
+    auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[t].y), __float_as_uint(v[t + 2].y), false, false);
+#ifdef MC_PERMLANE_NOP
+    asm volatile("s_nop 4" : "+v"(rx[0]), "+v"(rx[1]), "+v"(ry[0]), "+v"(ry[1]));
+#endif
     v[t] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
   // bit 3: t = 0 <-> 1 and bit 2: s = 0 <-> 1 as bank-masked DPP adds (each half of a 16-lane row
@@ -447,6 +475,9 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
     // ---- sub-tiles in reverse
 #pragma unroll 1
     for (int s = nsub - 1; s >= 0; --s) {
+#ifdef MC_BWD_VM0
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // diagnostic: every VMEM op retired before the rows are read
+#endif
       const uint2 ru = nu, rz = nz, rg = ng;
       const uint2 rd = kPD ? *reinterpret_cast<const uint2*>(dlt + (my_r * kS + kQT * s + 4 * h) * 2) : nd;
       // next step; after s = 0 the next chunk's first step (full chunk: its last sub-tile when fine)

@@ -195,27 +195,31 @@ __device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
   const f32x2 lg = f32x2{fast_log2(tp.x), fast_log2(tp.y)};
   return lg * kLn2 + f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
 }
-// MC_ASM_TAIL: appended to the arithmetic inline asm of the scan kernels.  Empty in the product build;
-// "s_nop 4" in the hazard-audit build (make ASM_AUDIT=1), which gives every asm result 5 wait states
-// before any consumer, whatever the compiler's hazard recognizer assumed about the opaque block.
+// MC_ASM_TAIL / MC_ASM_HEAD: appended / prepended to the arithmetic inline asm of the scan kernels.  Empty
+// in the product build; "s_nop 4" in the hazard-audit builds (make ASM_AUDIT=1: tail, ASM_AUDIT=2: both),
+// which give every asm result (and every asm operand) 5 wait states whatever the compiler's hazard
+// recognizer assumed about the opaque block.
 #ifndef MC_ASM_TAIL
 #define MC_ASM_TAIL ""
+#endif
+#ifndef MC_ASM_HEAD
+#define MC_ASM_HEAD ""
 #endif
 // a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
 // (the compiler otherwise moves an odd-register scalar to an even register first)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
   f32x2 r;
-  if constexpr (kHi) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
-  else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
+  if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
+  else asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
   return r;
 }
 // a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
   f32x2 r;
-  if constexpr (kHi) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
-  else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
+  else asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
   return r;
 }
 // exp2 of two values on the packed-FMA pipe (no transcendental): round-to-nearest split x = j + f

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--call", type=int, default=0, help="which scan backward of the step to wrap (0 = layer 23)")
     ap.add_argument("--concurrent", type=int, default=1)
     ap.add_argument("--pre-clone", action="store_true", help="also clone the inputs right BEFORE the call")
+    ap.add_argument("--generic", action="store_true",
+                    help="every scan backward of the step on the generic kernel (B / C passed as fp32)")
     args = ap.parse_args()
 
     from mamba_clip_amd import selective_scan_interface as ssi
@@ -58,13 +60,28 @@ def main():
     def cl(x):
         return x.detach().clone() if isinstance(x, torch.Tensor) else x
 
+    def generic_bwd(*a, **k):
+        a = list(a)
+        dt = a[3].dtype
+        a[3], a[4] = a[3].float(), a[4].float()
+        dbc = k.pop("dbc_out", None)
+        du, dd, dA, dB, dC, dD, dz, db = real_bwd(*a, **k)
+        dB, dC = dB.to(dt), dC.to(dt)
+        if dbc is not None:
+            dbc[0].copy_(dB)
+            dbc[1].copy_(dC)
+            dB, dC = dbc
+        return du, dd, dA, dB, dC, dD, dz, db
+
+    call_bwd = generic_bwd if args.generic else real_bwd
+
     def wrapped(*a, **k):
         i = state["n"]
         state["n"] += 1
         if i != args.call:
-            return real_bwd(*a, **k)
+            return call_bwd(*a, **k)
         pre = tuple(cl(x) for x in a) if args.pre_clone else None
-        out = real_bwd(*a, **k)
+        out = call_bwd(*a, **k)
         state["rec"] = {"ins": tuple(cl(x) for x in a), "outs": tuple(cl(x) for x in out), "pre": pre,
                         "stream": torch.cuda.current_stream().cuda_stream}
         return out
@@ -83,13 +100,13 @@ def main():
         torch.cuda.synchronize()
         rec = state["rec"]
         ins = rec["ins"]
-        solo = [real_bwd(*ins) for _ in range(2)]
+        solo = [call_bwd(*ins) for _ in range(2)]
         torch.cuda.synchronize()
         rec["solo"] = [tuple(cl(x) for x in s) for s in solo]
         rec["grads"] = {"dt_proj.bias": L23.dt_proj.bias.grad.clone(), "dt_proj.weight": L23.dt_proj.weight.grad.clone(),
                         "D": L23.D.grad.clone(), "A_log": L23.A_log.grad.clone(),
                         "x_proj.weight": L23.x_proj.weight.grad.clone(), "out_proj.weight": L23.out_proj.weight.grad.clone()}
-        rec["loss"] = float(loss)
+        rec["loss"] = float(loss.detach())
         runs.append(rec)
         line = {"run": r, "loss": rec["loss"], "n_scan_bwd": state["n"]}
 
@@ -107,6 +124,18 @@ def main():
         if args.pre_clone:
             line["inputs_changed_during_call"] = [IN_NAMES[j] for j, (x, y) in enumerate(zip(rec["pre"], ins))
                                                   if isinstance(x, torch.Tensor) and not eqt(x, y)]
+        cnt = lambda t: dict(sorted(collections.Counter(t.tolist()).items())[:40])
+        for j, nm in ((0, "du"), (6, "dz")):
+            x, y = rec["outs"][j], rec["solo"][0][j]
+            if isinstance(x, torch.Tensor) and not eqt(x, y):
+                idx = (x != y).nonzero()
+                line[nm + "_diff_channel_in_wave"] = cnt(idx[:, 1] % 32)
+                line[nm + "_diff_chunk"] = cnt(idx[:, 2] // 32)
+        x, y = rec["outs"][2], rec["solo"][0][2]
+        if not eqt(x, y):   # dA (dim, N)
+            idx = (x != y).nonzero()
+            line["dA_diff_channel_in_wave"] = cnt(idx[:, 0] % 32)
+            line["dA_diff_state"] = cnt(idx[:, 1])
         dd_x, dd_y = rec["outs"][1], rec["solo"][0][1]
         if not eqt(dd_x, dd_y):
             idx = (dd_x != dd_y).nonzero()
