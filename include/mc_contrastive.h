@@ -51,6 +51,15 @@ typedef struct mc_gemm_nt_params {
 
 int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream);
 
+/* Which kernel mc_gemm_nt runs for p (no launch): MC_GEMM_KERNEL_TILE (128 x 128 tiles, bf16 / fp32 /
+ * fp8 with K % 16), MC_GEMM_KERNEL_FP8_TILE (fp8, K % 128, block-scaled 16x16x128 MFMA tiles) or
+ * MC_GEMM_KERNEL_FP8_PANEL (fp8, K % 64 and K <= 512, N % 8, ldc % 8, 16-B aligned C: the register-panel
+ * kernel that serves the C5 similarity).  0 for an empty problem. */
+#define MC_GEMM_KERNEL_TILE 1
+#define MC_GEMM_KERNEL_FP8_TILE 2
+#define MC_GEMM_KERNEL_FP8_PANEL 3
+int32_t mc_gemm_nt_kernel(const mc_gemm_nt_params* p);
+
 /* Row-wise fp8 quantisation of a rows x cols matrix X (fp32 / bf16 / f16,
  * leading dimension ldx) for the fp8 similarity GEMM (stage-2 / frozen
  * features, BASELINE config 5):

@@ -23,6 +23,7 @@
 //  * ce_grad: fused softmax-minus-onehot gradient for the row and column CE
 //    terms in one pass, plus the logit_scale gradient sum(G*S)/scale.
 #include <algorithm>
+#include <cstdlib>
 
 #include "mc_common.h"
 #include "../../include/mc_contrastive.h"
@@ -696,6 +697,183 @@ __global__ __launch_bounds__(256, 2) void sim_fp8_kernel(const GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ fp8 similarity, panel kernel (round 6)
+// The C5 shape (K = E <= 512) has 4 MFMA K-steps of 128 bytes per output tile: sim_fp8_kernel's
+// 128 x 128 tiles re-stream both operands from L2 for every tile (537 MB of LDS-DMA per call at
+// N = 8192) and expose each tile's epilogue.  Here a workgroup (8 waves, one per CU) owns a 256-row
+// PANEL of A and a range of 64-column tiles of B:
+//  * the panel lives in registers for the whole launch: wave w keeps rows 64 (w & 3) .. +63 as
+//    v_mfma_scale_f32_32x32x64_f8f6f4 B-operand fragments (2 row blocks x K/64 steps x 32 B per lane =
+//    128 VGPRs at K = 512); A is read once per panel and n-range (32 MB at C5 instead of 268 MB);
+//  * B tiles (64 rows x K bytes) stream through a two-stage LDS image by LDS-DMA, one tile ahead,
+//    retired by a counted vmcnt and one raw s_barrier per tile (the swizzle sits on the source chunk,
+//    slot = chunk ^ (row & 15): a fragment read of 8 consecutive rows hits 8 distinct bank groups);
+//  * waves 0-3 take tile columns 0-31, waves 4-7 columns 32-63: 2 x 1 MFMAs of 32 x 32 per K-step,
+//    with the B tile as the MFMA's A operand so each lane ends with 4 consecutive COLUMNS of one output
+//    row per accumulator group (C^T orientation);
+//  * epilogue through a per-wave LDS block (row stride 36 floats: conflict-free 16-B writes and reads),
+//    scaled by the row factor (registers) and alpha x the column factor (LDS, loaded once), written as
+//    whole 128-B (fp32) / 64-B (bf16) row pieces with buffer stores -- always the same number of store
+//    instructions per tile (masked lanes address past the buffer), so the next tile's vmcnt is static;
+//    the stores stay in flight under the next tile's MFMAs (two waves per SIMD).
+// Grid: one workgroup per (panel, n-range), n-ranges sized for ~256 workgroups; consecutive logical
+// workgroups (xcd_remap) share an n-range, so one XCD's L2 serves that range's B tiles to its panels.
+constexpr int kP8Rows = 256;                 // panel rows per workgroup
+constexpr int kP8Cols = 64;                  // B tile columns
+constexpr int kP8Row = 512;                  // LDS bytes per B row (K <= 512)
+constexpr int kP8Stage = kP8Cols * kP8Row;   // 32 KB
+constexpr int kP8EpStride = 36;              // floats per staged output row (32 + 4 pad)
+constexpr int kP8EpWave = 64 * kP8EpStride;  // floats per wave
+constexpr int kP8MaxTiles = 32;              // tiles per workgroup (column factors held in LDS)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename TOut, int NKS>
+__global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, int nr, int tpr) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kP8Stage + 8 * kP8EpWave * 4 + kP8MaxTiles * kP8Cols * 4];
+  float* ep_all = reinterpret_cast<float*>(lds + 2 * kP8Stage);
+  float* colf = ep_all + 8 * kP8EpWave;        // alpha * column factor of the workgroup's columns
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = w & 3, cg = w >> 2;
+  const int lin = xcd_remap(blockIdx.x, g.tiles_m * nr);
+  const int nrange = lin / g.tiles_m, panel = lin % g.tiles_m;
+  const int m0 = panel * kP8Rows;
+  const int ntiles = (g.N + kP8Cols - 1) / kP8Cols;
+  const int t0 = nrange * tpr, t1 = min(ntiles, t0 + tpr);
+  if (t0 >= t1) return;   // uniform across the workgroup
+  const uint8_t* __restrict__ A = reinterpret_cast<const uint8_t*>(g.A);
+  const uint8_t* __restrict__ B = reinterpret_cast<const uint8_t*>(g.B);
+  constexpr int kChunks = 4 * NKS;             // 16-B chunks of a row (K = 64 NKS bytes)
+
+  // ---- A panel fragments (B operand of the MFMA: lane = row l & 31, K bytes [32 (l >> 5), +32) per step)
+  i32x8 af[2][NKS];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int row = min(m0 + rg * 64 + rb * 32 + (lane & 31), g.M - 1);
+    const uint8_t* ap = A + (int64_t)row * g.lda + 32 * (lane >> 5);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const uint4 lo = *reinterpret_cast<const uint4*>(ap + ks * 64);
+      const uint4 hi = *reinterpret_cast<const uint4*>(ap + ks * 64 + 16);
+      af[rb][ks] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+  }
+  // ---- row factors of the rows this lane writes in the epilogue; column factors (x alpha) -> LDS
+  constexpr int kRowsPerStore = sizeof(TOut) == 4 ? 8 : 16;       // output rows per store instruction
+  constexpr int kStores = 64 / kRowsPerStore;                     // store instructions per tile and wave
+  const int er = sizeof(TOut) == 4 ? (lane >> 3) : (lane >> 2);   // row within a store's row group
+  const int ec = sizeof(TOut) == 4 ? 4 * (lane & 7) : 8 * (lane & 3);   // first column (of the wave's 32)
+  float rsf[kStores];
+#pragma unroll
+  for (int j = 0; j < kStores; ++j) {
+    const int m = m0 + rg * 64 + j * kRowsPerStore + er;
+    rsf[j] = (g.sa && m < g.M) ? g.sa[m] : 1.f;
+  }
+  {
+    const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
+    const int ncols = (t1 - t0) * kP8Cols;
+    for (int i = tid; i < ncols; i += 512) {
+      const int n = t0 * kP8Cols + i;
+      colf[i] = alpha * ((g.sb && n < g.N) ? g.sb[n] : 1.f);
+    }
+  }
+
+  // ---- B tile LDS-DMA: wave w, instruction j, lane l -> chunk q = (4w + j) * 64 + l of the 64 x 32-chunk image
+  int boff[4];
+  const int bslot0 = w * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = (bslot0 + j) * 64 + lane, r = q >> 5, slot = q & 31;
+    boff[j] = min(slot ^ (r & 15), kChunks - 1) * 16;   // chunks past K: a valid chunk, never read
+  }
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_char*)(lds));
+  auto issue = [&](int tile, int st) __attribute__((always_inline)) {
+    const int n0 = tile * kP8Cols;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = (bslot0 + j) * 64 + lane, r = q >> 5;
+      const uint8_t* src = B + (int64_t)min(n0 + r, g.N - 1) * g.ldb + boff[j];
+      glds16_asm(src, lds_base + st * kP8Stage + (bslot0 + j) * 1024);
+    }
+  };
+
+  // ---- output: one buffer resource over this wave's 64 rows (masked lanes address past its end)
+  TOut* __restrict__ C = reinterpret_cast<TOut*>(g.C);
+  const int wrow0 = m0 + rg * 64;
+  const int wrows = max(0, min(64, g.M - wrow0));
+  const __amdgpu_buffer_rsrc_t rc =
+      make_rsrc(C + (int64_t)min(wrow0, g.M - 1) * g.ldc,
+                wrows > 0 ? (uint32_t)(((int64_t)(wrows - 1) * g.ldc + g.N) * (int64_t)sizeof(TOut)) : 0u);
+  float* ep = ep_all + w * kP8EpWave;
+  const int nl = cg * 32 + (lane & 31);        // this lane's B row (tile column) in the fragment reads
+
+  issue(t0, 0);
+  for (int t = t0; t < t1; ++t) {
+    const int st = (t - t0) & 1;
+    // this wave's DMA of tile t landed (the previous tile's kStores stores may stay in flight), this
+    // wave's LDS reads of tile t - 1 are done, then everyone's: stage st is readable, st ^ 1 is free
+    if (t == t0) __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+    else if constexpr (kStores == 8) __builtin_amdgcn_s_waitcnt(0x0078);   // vmcnt(8) lgkmcnt(0)
+    else __builtin_amdgcn_s_waitcnt(0x0074);                                // vmcnt(4) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < t1) issue(t + 1, st ^ 1);
+    asm volatile("" ::: "memory");
+
+    const char* sb = lds + st * kP8Stage + nl * kP8Row;
+    const int sw = nl & 15;
+    f32x16 acc0 = {}, acc1 = {};
+    auto bfrag = [&](int ks) __attribute__((always_inline)) {
+      const int c0 = 4 * ks + 2 * (lane >> 5);
+      const uint4 b0 = *reinterpret_cast<const uint4*>(sb + ((c0 ^ sw) << 4));
+      const uint4 b1 = *reinterpret_cast<const uint4*>(sb + (((c0 + 1) ^ sw) << 4));
+      return i32x8{(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+    };
+    i32x8 bf = bfrag(0);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const i32x8 bcur = bf;
+      if (ks + 1 < NKS) bf = bfrag(ks + 1);   // next fragment's LDS reads under this step's MFMAs
+      acc0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bcur, af[0][ks], acc0, 0, 0, 0, 127, 0, 127);
+      acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bcur, af[1][ks], acc1, 0, 0, 0, 127, 0, 127);
+    }
+    // ---- epilogue: C^T fragments -> this wave's LDS block [64 rows][32 cols] (row m = l & 31 of block rb,
+    // columns 8 i + 4 (l >> 5) + [0, 4))
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = 8 * i + 4 * (lane >> 5);
+      *reinterpret_cast<f32x4*>(ep + (lane & 31) * kP8EpStride + col) =
+          f32x4{acc0[4 * i], acc0[4 * i + 1], acc0[4 * i + 2], acc0[4 * i + 3]};
+      *reinterpret_cast<f32x4*>(ep + (32 + (lane & 31)) * kP8EpStride + col) =
+          f32x4{acc1[4 * i], acc1[4 * i + 1], acc1[4 * i + 2], acc1[4 * i + 3]};
+    }
+    asm volatile("" ::: "memory");   // one wave's LDS operations run in program order
+    const int n_w = t * kP8Cols + cg * 32 + ec;                       // first output column of this lane
+    const float* cf = colf + (t - t0) * kP8Cols + cg * 32 + ec;
+    const bool col_ok = n_w < g.N;                                    // N % 8 == 0: whole vectors
+#pragma unroll
+    for (int j = 0; j < kStores; ++j) {
+      const int rl = j * kRowsPerStore + er;                          // row within the wave's 64
+      const bool ok = col_ok && rl < wrows;
+      const uint32_t off = ok ? (uint32_t)(((int64_t)rl * g.ldc + n_w) * (int64_t)sizeof(TOut)) : 0x80000000u;
+      if constexpr (sizeof(TOut) == 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ep + rl * kP8EpStride + ec);
+        const f32x4 c4 = *reinterpret_cast<const f32x4*>(cf);
+        const f32x4 o = (v * rsf[j]) * c4;
+        buf_st16(rc, off, make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
+                                     __float_as_uint(o[3])));
+      } else {
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + rl * kP8EpStride + ec);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + rl * kP8EpStride + ec + 4);
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(cf);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(cf + 4);
+        const f32x4 o0 = (v0 * rsf[j]) * c0, o1 = (v1 * rsf[j]) * c1;
+        buf_st16(rc, off, make_uint4(cvt_pk2<TOut>(o0[0], o0[1]), cvt_pk2<TOut>(o0[2], o0[3]),
+                                     cvt_pk2<TOut>(o1[0], o1[1]), cvt_pk2<TOut>(o1[2], o1[3])));
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ CE statistics
 
 // one wave per row: lse and nll, per-block partial NLL sums (4 rows per block)
@@ -930,6 +1108,41 @@ void launch_gemm(const GemmArgs& g, int in_dtype, int out_dtype, bool aligned, h
 #undef MC_GEMM
 }
 
+// The panel kernel's eligibility: K % 64 == 0, K <= 512; whole 16-B output vectors (N % 8, ldc % 8 and a
+// 16-B aligned C); 32-bit buffer offsets over the output.  MAMBA_CLIP_AMD_SIM8_PANEL=0 keeps the
+// 128 x 128 tile kernel (A/B).
+bool sim8_panel_ok(const GemmArgs& g, const mc_gemm_nt_params* p) {
+  static const bool on = [] {
+    const char* e = getenv("MAMBA_CLIP_AMD_SIM8_PANEL");
+    return !(e && e[0] == '0');
+  }();
+  const int es = p->out_dtype == MC_DTYPE_F32 ? 4 : 2;
+  return on && p->K > 0 && p->K % 64 == 0 && p->K <= kP8Row && p->N % 8 == 0 && p->ldc % 8 == 0 && aligned16(p->C) &&
+         (int64_t)p->M * p->ldc * es < ((int64_t)1 << 31);
+}
+
+template <typename TOut>
+void launch_sim8_panel_t(const GemmArgs& g0, hipStream_t s) {
+  GemmArgs g = g0;
+  g.tiles_m = (g.M + kP8Rows - 1) / kP8Rows;   // panels
+  const int ntiles = (g.N + kP8Cols - 1) / kP8Cols;
+  int nr = std::max((256 + g.tiles_m - 1) / g.tiles_m, (ntiles + kP8MaxTiles - 1) / kP8MaxTiles);
+  nr = std::min(nr, ntiles);
+  const int tpr = (ntiles + nr - 1) / nr;
+  nr = (ntiles + tpr - 1) / tpr;               // no empty n-ranges
+  const dim3 grid(g.tiles_m * nr), block(512);
+  switch (g.K / 64) {
+#define MC_P8(NK) case NK: hipLaunchKernelGGL((sim8_panel_kernel<TOut, NK>), grid, block, 0, s, g, nr, tpr); break;
+    MC_P8(1) MC_P8(2) MC_P8(3) MC_P8(4) MC_P8(5) MC_P8(6) MC_P8(7) MC_P8(8)
+#undef MC_P8
+    default: break;
+  }
+}
+void launch_sim8_panel(const GemmArgs& g, int out_dtype, hipStream_t s) {
+  if (out_dtype == MC_DTYPE_F32) launch_sim8_panel_t<float>(g, s);
+  else launch_sim8_panel_t<bf16_t>(g, s);
+}
+
 // shape / alignment checks shared by the plain GEMM and the fused CE entry points
 int fill_operands(GemmArgs& g, const char* who, int M, int N, int K, int in_dtype, const void* A, int64_t lda,
                   const void* B, int64_t ldb, bool& aligned) {
@@ -952,6 +1165,17 @@ int fill_operands(GemmArgs& g, const char* who, int M, int N, int K, int in_dtyp
 }
 }  // namespace
 
+extern "C" int32_t mc_gemm_nt_kernel(const mc_gemm_nt_params* p) {
+  if (!p || p->M <= 0 || p->N <= 0) return 0;
+  GemmArgs g;
+  bool aligned;
+  if (fill_operands(g, "mc_gemm_nt_kernel", p->M, p->N, p->K, p->in_dtype, p->A, p->lda, p->B, p->ldb, aligned) != MC_OK)
+    return 0;
+  if (p->in_dtype == MC_DTYPE_FP8_E4M3 && sim8_panel_ok(g, p)) return MC_GEMM_KERNEL_FP8_PANEL;
+  if (p->in_dtype == MC_DTYPE_FP8_E4M3 && p->K % kSBK == 0 && p->K > 0) return MC_GEMM_KERNEL_FP8_TILE;
+  return MC_GEMM_KERNEL_TILE;
+}
+
 extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_gemm_nt: null params");
   MC_CHECK(p->M >= 0 && p->N >= 0 && p->K >= 0, MC_ERR_SHAPE, "mc_gemm_nt: negative shape");
@@ -970,7 +1194,9 @@ extern "C" int mc_gemm_nt(const mc_gemm_nt_params* p, void* stream) {
   g.sa = p->row_scale_a; g.sb = p->row_scale_b;
   g.c_vec = aligned16(p->C) && p->ldc % 4 == 0;
   g.c_vec16 = g.c_vec && p->ldc % 8 == 0;
-  if (p->in_dtype == MC_DTYPE_FP8_E4M3 && p->K % kSBK == 0 && p->K > 0) {   // the C5 similarity path
+  if (p->in_dtype == MC_DTYPE_FP8_E4M3 && sim8_panel_ok(g, p)) {   // the C5 similarity path (K <= 512)
+    launch_sim8_panel(g, p->out_dtype, (hipStream_t)stream);
+  } else if (p->in_dtype == MC_DTYPE_FP8_E4M3 && p->K % kSBK == 0 && p->K > 0) {   // fp8, longer K
     const dim3 grid(g.tiles_m * g.tiles_n), block(256);
     if (p->out_dtype == MC_DTYPE_F32) hipLaunchKernelGGL(sim_fp8_kernel<float>, grid, block, 0, (hipStream_t)stream, g);
     else hipLaunchKernelGGL(sim_fp8_kernel<bf16_t>, grid, block, 0, (hipStream_t)stream, g);

@@ -151,6 +151,23 @@ __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
   // >= 2 wait states between the last product and the first swap (tools/hazard_scan.py).
   asm volatile("s_nop 1" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                "+v"(v[7]));
+#ifdef MC_BWD_BPERMUTE   // diagnostic: the two cross-row halvings through ds_bpermute, no permlane swaps
+  {
+    const bool up32 = lane & 32, up16 = lane & 16;
+    const int p32 = (lane ^ 32) << 2, p16 = (lane ^ 16) << 2;
+    auto xch = [](int addr, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v))); };
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f32x2 keep = up32 ? v[t + 4] : v[t], send = up32 ? v[t] : v[t + 4];
+      v[t] = keep + f32x2{xch(p32, send.x), xch(p32, send.y)};
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x2 keep = up16 ? v[t + 2] : v[t], send = up16 ? v[t] : v[t + 2];
+      v[t] = keep + f32x2{xch(p16, send.x), xch(p16, send.y)};
+    }
+  }
+#else
 #pragma unroll
   for (int t = 0; t < 4; ++t) {   // bit 5: t <-> t + 4
     auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t + 4].x), false, false);
@@ -169,6 +186,7 @@ __device__ __forceinline__ float pair_reduce16(f32x2 (&v)[8], int lane) {
 #endif
     v[t] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
+#endif
   // bit 3: t = 0 <-> 1 and bit 2: s = 0 <-> 1 as bank-masked DPP adds (each half of a 16-lane row
   // writes its own sum), instead of keep / send selects around a DPP move
   const float x = halve_bit3(v[0].x, v[1].x), y = halve_bit3(v[0].y, v[1].y);
@@ -198,6 +216,13 @@ __device__ __forceinline__ f32x2 elem2(uint2 w, int i) {   // elements 2i, 2i + 
   const uint4 q = make_uint4(w.x, w.y, 0u, 0u);
   return f32x2{elem_f<TI>(q, 2 * i), elem_f<TI>(q, 2 * i + 1)};
 }
+
+#ifdef MC_BWD_DEBUG
+// Diagnostic build only: per (workgroup, wave, chunk, sub-tile, lane) snapshots of the reverse
+// sweep's carries, written to a library-owned buffer that the host copies out (mc_debug_copy).
+__device__ float* g_dbg = nullptr;
+constexpr int kDbgVals = 32;   // floats per lane and sub-tile: hcar[4] (8), dA2[4] (8), A2[4] (8), entry state (8)
+#endif
 
 template <typename TI, bool kSP, bool kZ, bool kPD, bool kFine>
 __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPairArgs a) {
@@ -512,7 +537,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
 #pragma unroll
         for (int t = 0; t < kQT; ++t) {
           const f32x2 arg = (t & 1) ? pk_mul_bcast<1>(a2p, sc.dt[t >> 1]) : pk_mul_bcast<0>(a2p, sc.dt[t >> 1]);
-          as[t] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
+          as[t] = f32x2{pexp2(arg.x), pexp2(arg.y)};
         }
         {   // (B dt u off the chain: one pk_fma per step on it)
           f32x2 x = xin;
@@ -520,7 +545,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
           for (int t = 0; t < kQT; ++t) {
             const f32x2 bb = bpair(kQT * s + t, p);
             const f32x2 bu = (t & 1) ? pk_mul_bcast<1>(bb, sc.dtu[t >> 1]) : pk_mul_bcast<0>(bb, sc.dtu[t >> 1]);
-            x = as[t] * x + bu;
+            x = pfma(as[t], x, bu);
             xs[t] = x;
           }
         }
@@ -546,12 +571,12 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
             if (t > 0) qn = bquad(kQT * s + t - 1, p);
             lam = (t & 1) ? pk_fma_bcast<1>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha)
                           : pk_fma_bcast<0>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha);
-            if (hasZ) Y2[t] = q.hi * xs[t] + Y2[t];
-            S2[t] = lam * q.lo + S2[t];
+            if (hasZ) Y2[t] = pfma(q.hi, xs[t], Y2[t]);
+            S2[t] = pfma(lam, q.lo, S2[t]);
             red[t] = (t & 1) ? pk_mul_bcast<1>(lam, sc.dtu[t >> 1]) : pk_mul_bcast<0>(lam, sc.dtu[t >> 1]);
-            ha = lam * as[t];
-            const f32x2 hax = ha * (t > 0 ? xs[t - 1] : xin);
-            Q2[t] = hax * a2p + Q2[t];
+            ha = pmul(lam, as[t]);
+            const f32x2 hax = pmul(ha, t > 0 ? xs[t - 1] : xin);
+            Q2[t] = pfma(hax, a2p, Q2[t]);
             dap = (t & 1) ? pk_fma_bcast<1>(hax, sc.dt[t >> 1], dap) : pk_fma_bcast<0>(hax, sc.dt[t >> 1], dap);
           }
           asm volatile("" : "+v"(ha), "+v"(dap));
@@ -608,6 +633,20 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
           dbacc += dd.x + dd.y;
         }
       }
+#ifdef MC_BWD_DEBUG
+      if (g_dbg) {
+        const int nch_ = (L_ + kS - 1) / kS;
+        float* d = g_dbg + ((((int64_t)lin * kQW + wave) * nch_ + c) * kQSub + s) * 64 * kDbgVals + lane * kDbgVals;
+#pragma unroll
+        for (int p = 0; p < kQP; ++p) {
+          d[2 * p] = hcar[p].x; d[2 * p + 1] = hcar[p].y;
+          d[8 + 2 * p] = dA2[p].x; d[8 + 2 * p + 1] = dA2[p].y;
+          d[16 + 2 * p] = A2[p].x; d[16 + 2 * p + 1] = A2[p].y;
+        }
+        d[24] = xi01.x; d[25] = xi01.y; d[26] = xi01.z; d[27] = xi01.w;
+        d[28] = xi23.x; d[29] = xi23.y; d[30] = xi23.z; d[31] = xi23.w;
+      }
+#endif
       const uint32_t e0 = (uint32_t)(l0 + kQT * s + 4 * h);
       buf_st8(rs_du, ((ro_du + e0) * 2u) | st_mask, make_uint2(cvt_pk2<TI>(o_du[0], o_du[1]), cvt_pk2<TI>(o_du[2], o_du[3])));
       buf_st8(rs_dd, ((ro_dd + e0) * 2u) | st_mask, make_uint2(cvt_pk2<TI>(o_dd[0], o_dd[1]), cvt_pk2<TI>(o_dd[2], o_dd[3])));
@@ -733,3 +772,23 @@ void launch_bwd_pair(const mc_scan_bwd_params* p, float* slab_bc, float* slab_a,
 
 }  // namespace scan
 }  // namespace mc
+
+#ifdef MC_BWD_DEBUG
+extern "C" int mc_debug_alloc(size_t bytes) {
+  static float* buf = nullptr;
+  static size_t have = 0;
+  if (bytes > have) {
+    if (buf) (void)hipFree(buf);
+    if (hipMalloc(&buf, bytes) != hipSuccess) return 1;
+    have = bytes;
+  }
+  (void)hipMemset(buf, 0, bytes);
+  float* p = bytes ? buf : nullptr;
+  return hipMemcpyToSymbol(HIP_SYMBOL(mc::scan::g_dbg), &p, sizeof(p)) == hipSuccess ? 0 : 2;
+}
+extern "C" int mc_debug_copy(void* dst, size_t bytes, void* stream) {
+  float* p = nullptr;
+  if (hipMemcpyFromSymbol(&p, HIP_SYMBOL(mc::scan::g_dbg), sizeof(p)) != hipSuccess || !p) return 1;
+  return hipMemcpyAsync(dst, p, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream) == hipSuccess ? 0 : 2;
+}
+#endif

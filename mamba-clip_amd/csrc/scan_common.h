@@ -205,10 +205,52 @@ __device__ __forceinline__ f32x2 softplus2_log1p(f32x2 x) {
 #ifndef MC_ASM_HEAD
 #define MC_ASM_HEAD ""
 #endif
+// Packed / transcendental arithmetic of the pair backward's sweeps.  Plain expressions in the product
+// build; with MC_PK_PAD / MC_EXP_PAD (diagnostic) each is an asm op followed by "s_nop N", so
+// every result has that many extra wait states before its first consumer whatever the compiler scheduled.
+#if defined(MC_SCALAR_PK)   // diagnostic: every sweep product as two scalar VALU ops, no packed math
+__device__ __forceinline__ f32x2 pmul(f32x2 a, f32x2 b) {
+  float x, y;
+  asm("v_mul_f32 %0, %2, %3\n\tv_mul_f32 %1, %4, %5" : "=&v"(x), "=&v"(y) : "v"(a.x), "v"(b.x), "v"(a.y), "v"(b.y));
+  return f32x2{x, y};
+}
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) {
+  float x, y;
+  asm("v_fma_f32 %0, %2, %3, %4\n\tv_fma_f32 %1, %5, %6, %7" : "=&v"(x), "=&v"(y)
+      : "v"(a.x), "v"(b.x), "v"(c.x), "v"(a.y), "v"(b.y), "v"(c.y));
+  return f32x2{x, y};
+}
+#elif defined(MC_PK_PAD)
+__device__ __forceinline__ f32x2 pmul(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_mul_f32 %0, %1, %2\n\ts_nop " MC_PK_PAD : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3\n\ts_nop " MC_PK_PAD : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+#else
+__device__ __forceinline__ f32x2 pmul(f32x2 a, f32x2 b) { return a * b; }
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return a * b + c; }
+#endif
+#ifdef MC_EXP_PAD   // (the leading nop covers the VALU -> trans operand read the compiler cannot see into)
+__device__ __forceinline__ float pexp2(float a) {
+  float r;
+  asm("s_nop 1\n\tv_exp_f32 %0, %1\n\ts_nop " MC_EXP_PAD : "=v"(r) : "v"(a));
+  return r;
+}
+#else
+__device__ __forceinline__ float pexp2(float a) { return fast_exp2(a); }
+#endif
 // a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
 // (the compiler otherwise moves an odd-register scalar to an even register first)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
+#ifdef MC_SCALAR_PK
+  return pmul(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x});
+#endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
   else asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
@@ -217,6 +259,9 @@ __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
 // a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
+#ifdef MC_SCALAR_PK
+  return pfma(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x}, c);
+#endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
   else asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));

@@ -16,6 +16,7 @@ MC_LAYOUT_NCHW, MC_LAYOUT_NHWC = 0, 1
 MC_SCAN_CHUNK = 32
 MC_SCAN_STATE_INTERVAL_FINE = 8
 MC_SCAN_KERNEL_NONE, MC_SCAN_KERNEL_PAIR, MC_SCAN_KERNEL_GENERIC, MC_SCAN_KERNEL_DIRS = 0, 1, 2, 3
+MC_GEMM_KERNEL_TILE, MC_GEMM_KERNEL_FP8_TILE, MC_GEMM_KERNEL_FP8_PANEL = 1, 2, 3   # mc_gemm_nt_kernel
 MC_SCAN_MAX_DSTATE = 32
 MC_CAST_CHUNK = 16384
 
@@ -256,6 +257,7 @@ SYMBOLS = {
     "mc_scan_fwd": (ctypes.c_int, [ctypes.POINTER(ScanFwdParams), c_vp]),
     "mc_scan_bwd": (ctypes.c_int, [ctypes.POINTER(ScanBwdParams), c_vp]),
     "mc_gemm_nt": (ctypes.c_int, [ctypes.POINTER(GemmNTParams), c_vp]),
+    "mc_gemm_nt_kernel": (c_i32, [ctypes.POINTER(GemmNTParams)]),
     "mc_quant_rows_fp8": (ctypes.c_int, [c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_fp, c_vp]),
     "mc_ce_stats": (ctypes.c_int, [c_i32, c_i32, c_fp, c_i64, c_i32, c_i64, c_fp, c_fp, ctypes.c_float, c_fp,
                                    c_vp, ctypes.c_size_t, c_vp]),

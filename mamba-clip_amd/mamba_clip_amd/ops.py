@@ -59,8 +59,14 @@ def gemm_nt(A, B, alpha=1.0, alpha_dev=None, out_dtype=torch.float32, scale_a=No
             if sc.dtype != torch.float32 or sc.numel() != n or not sc.is_contiguous():
                 raise RuntimeError(f"gemm_nt: {name} must be a contiguous fp32 vector of {n} entries")
             setattr(p, name, sc.data_ptr())
+    if GEMM_NT_RECORD is not None:
+        GEMM_NT_RECORD.append(int(lib.mc_gemm_nt_kernel(p)))
     _lib.check(lib.mc_gemm_nt(p, _lib.stream_handle(A.device)), "mc_gemm_nt")
     return C
+
+
+# Tests set GEMM_NT_RECORD = [] to see which kernel each gemm_nt call ran (_lib.MC_GEMM_KERNEL_*).
+GEMM_NT_RECORD = None
 
 
 def quant_rows_fp8(X):
@@ -90,27 +96,16 @@ def similarity_fp8(image_features, text_features, logit_scale, out_dtype=torch.f
 
     The similarity matmul of ClipModel.get_logits (model.py:1104-1112) on
     frozen features, fp8 MFMA (BASELINE config 5).  ``logit_scale`` is the
-    already-exponentiated scale (a 0-d device tensor or a float).
+    already-exponentiated scale (a 0-d device tensor or a float).  fp32 or bf16
+    logits, both on the library's own kernels (mc_gemm_nt: the register-panel fp8
+    kernel for K <= 512); no vendor GEMM.
     """
     qi, si = quant_rows_fp8(image_features)
     qt, st = quant_rows_fp8(text_features)
-    if out_dtype == torch.bfloat16 and _rowwise_scaled_mm_ok(qi, qt):
-        # bf16 logits: hipBLASLt's row-wise scaled fp8 GEMM (torch._scaled_mm) measured faster than
-        # sim_fp8_kernel at C5 (59.7-60.4 vs 86.4 us, profiles/r04/c5_variants_dp.txt); alpha folds into
-        # the row factors.  hipBLASLt has no fp32-out row-wise kernel: fp32 logits stay on sim_fp8_kernel.
-        sa = (si * (logit_scale.reshape(()).float() if torch.is_tensor(logit_scale) else float(logit_scale)))
-        return torch._scaled_mm(qi, qt.t(), scale_a=sa.reshape(-1, 1), scale_b=st.reshape(1, -1),
-                                out_dtype=torch.bfloat16)
     if torch.is_tensor(logit_scale):
         return gemm_nt(qi, qt, alpha_dev=logit_scale.reshape(()).float().contiguous(), out_dtype=out_dtype,
                        scale_a=si, scale_b=st)
     return gemm_nt(qi, qt, alpha=float(logit_scale), out_dtype=out_dtype, scale_a=si, scale_b=st)
-
-
-def _rowwise_scaled_mm_ok(qi, qt):
-    """Shapes hipBLASLt's row-wise fp8 kernels take (K % 16, N % 16: qt.t() column-major, 16-B rows)."""
-    return (hasattr(torch, "_scaled_mm") and qi.shape[1] == qt.shape[1] and qi.shape[1] % 16 == 0
-            and qt.shape[0] % 16 == 0 and qi.shape[0] > 0)
 
 
 def clip_loss_fp8(image_features, text_features, logit_scale):

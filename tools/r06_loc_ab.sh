@@ -13,6 +13,7 @@ for v in ${VARIANTS:-permnop nogemm nowgrad}; do
     nogemm) run nogemm MAMBA_CLIP_AMD_WGRAD_HIP=0 MAMBA_CLIP_AMD_MLP_HIP_FC2=0 MAMBA_CLIP_AMD_MLP_HIP_BWD=0 MAMBA_CLIP_AMD_SMALL_K_HIP=0 ;;
     nowgrad) run nowgrad MAMBA_CLIP_AMD_WGRAD_HIP=0 ;;
     nomlp) run nomlp MAMBA_CLIP_AMD_MLP_HIP_FC2=0 MAMBA_CLIP_AMD_MLP_HIP_BWD=0 ;;
+    dbg) env MAMBA_CLIP_AMD_LIB=$PWD/$L/libmamba_clip_amd_v_dbg.so timeout -k 10 150 python3 -u tools/scan_bwd_localize.py --batch 32 --runs ${RUNS:-5} --debug > gpurun_out/r06_loc/g_dbg.log 2>&1 || exit 1 ;;
     *) run $v MAMBA_CLIP_AMD_LIB=$PWD/$L/libmamba_clip_amd_v_$v.so ;;
   esac
 done

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--call", type=int, default=0, help="which scan backward of the step to wrap (0 = layer 23)")
     ap.add_argument("--concurrent", type=int, default=1)
     ap.add_argument("--pre-clone", action="store_true", help="also clone the inputs right BEFORE the call")
+    ap.add_argument("--debug", action="store_true",
+                    help="diagnostic library (-DMC_BWD_DEBUG): compare the pair kernel's per-sub-tile carry snapshots")
     ap.add_argument("--generic", action="store_true",
                     help="every scan backward of the step on the generic kernel (B / C passed as fp32)")
     args = ap.parse_args()
@@ -74,6 +76,25 @@ def main():
         return du, dd, dA, dB, dC, dD, dz, db
 
     call_bwd = generic_bwd if args.generic else real_bwd
+    dbg = {}
+    if args.debug:
+        import ctypes
+        from mamba_clip_amd import _lib
+        lib = _lib.load()
+        lib.mc_debug_alloc.argtypes = [ctypes.c_size_t]
+        lib.mc_debug_copy.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        D_, L_ = 1536, 80
+        nblk, nch = (D_ + 127) // 128, (L_ + 31) // 32
+        dbg["shape"] = (args.batch * nblk, 4, nch, 4, 64, 32)
+        dbg["bytes"] = 4 * args.batch * nblk * 4 * nch * 4 * 64 * 32
+        assert lib.mc_debug_alloc(dbg["bytes"]) == 0
+        torch.cuda.synchronize()
+
+        def snap_dbg():
+            t = torch.empty(dbg["shape"], device=dev, dtype=torch.float32)
+            assert lib.mc_debug_copy(t.data_ptr(), dbg["bytes"], torch.cuda.current_stream().cuda_stream) == 0
+            return t
+        dbg["snap"] = snap_dbg
 
     def wrapped(*a, **k):
         i = state["n"]
@@ -83,7 +104,8 @@ def main():
         pre = tuple(cl(x) for x in a) if args.pre_clone else None
         out = call_bwd(*a, **k)
         state["rec"] = {"ins": tuple(cl(x) for x in a), "outs": tuple(cl(x) for x in out), "pre": pre,
-                        "stream": torch.cuda.current_stream().cuda_stream}
+                        "stream": torch.cuda.current_stream().cuda_stream,
+                        "dbg": dbg["snap"]() if args.debug else None}
         return out
 
     ssi.scan_bwd = wrapped
@@ -102,6 +124,48 @@ def main():
         ins = rec["ins"]
         solo = [call_bwd(*ins) for _ in range(2)]
         torch.cuda.synchronize()
+        if args.debug:
+            sd = dbg["snap"]()
+            torch.cuda.synchronize()
+            x = rec["dbg"]
+            bad = (x != sd)                                   # (blk, wave, c, s, lane, val)
+            if bool(bad.any()):
+                nb, nw, nc, ns = bad.shape[:4]
+                # processing order: chunks and sub-tiles descending
+                order = [(c, s_) for c in range(nc - 1, -1, -1) for s_ in range(ns - 1, -1, -1)]
+                firsts, lanes_first, vals_first = collections.Counter(), collections.Counter(), collections.Counter()
+                per_wave = bad.any(dim=5).any(dim=4)            # (blk, wave, c, s)
+                idx = per_wave.nonzero().tolist()
+                seen = {}
+                rank = {cs: i for i, cs in enumerate(order)}
+                for blk, w, c, s_ in idx:
+                    key = (blk, w)
+                    if key not in seen or rank[(c, s_)] < rank[seen[key]]:
+                        seen[key] = (c, s_)
+                for (blk, w), (c, s_) in seen.items():
+                    firsts[(c, s_)] += 1
+                    lb = bad[blk, w, c, s_]                     # (lane, val)
+                    for ln in lb.any(dim=1).nonzero().flatten().tolist():
+                        lanes_first[ln] += 1
+                    for v in lb.any(dim=0).nonzero().flatten().tolist():
+                        vals_first[v] += 1
+                waves_idx = collections.Counter(w for (blk, w) in seen)
+                blocks = sorted({blk for (blk, w) in seen})
+                # which quantities differ anywhere (not only at the first sub-tile): hcar 0-7, dA 8-15, A2 16-23, entry 24-31
+                anyv = bad.reshape(-1, 32).any(dim=0).nonzero().flatten().tolist()
+                line_dbg_extra = {"wave_index": dict(sorted(waves_idx.items())), "n_blocks": len(blocks),
+                                  "blocks_head": blocks[:24], "vals_anywhere": anyv}
+                line_dbg = {"waves_affected": len(seen), "first_cs": {f"{c},{s_}": n for (c, s_), n in sorted(firsts.items())},
+                            "first_lanes": dict(sorted(lanes_first.items())), "first_vals": dict(sorted(vals_first.items()))}
+                ex = next(iter(seen.items()))
+                (blk, w), (c, s_) = ex
+                ln = bad[blk, w, c, s_].any(dim=1).nonzero().flatten()[0].item()
+                line_dbg.update(line_dbg_extra)
+                line_dbg["example"] = {"blk": blk, "wave": w, "c": c, "s": s_, "lane": ln,
+                                       "instep": x[blk, w, c, s_, ln].tolist(), "solo": sd[blk, w, c, s_, ln].tolist()}
+            else:
+                line_dbg = {"waves_affected": 0}
+            rec["dbg_line"] = line_dbg
         rec["solo"] = [tuple(cl(x) for x in s) for s in solo]
         rec["grads"] = {"dt_proj.bias": L23.dt_proj.bias.grad.clone(), "dt_proj.weight": L23.dt_proj.weight.grad.clone(),
                         "D": L23.D.grad.clone(), "A_log": L23.A_log.grad.clone(),
@@ -109,6 +173,9 @@ def main():
         rec["loss"] = float(loss.detach())
         runs.append(rec)
         line = {"run": r, "loss": rec["loss"], "n_scan_bwd": state["n"]}
+        if args.debug:
+            line["dbg"] = rec.pop("dbg_line")
+            rec["dbg"] = None
 
         def eqt(x, y):
             if isinstance(x, torch.Tensor):
