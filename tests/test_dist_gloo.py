@@ -278,6 +278,79 @@ def _ddp_streams_worker(rank, world, port, q):
         q.put((rank, {"error": repr(e) + traceback.format_exc()}))
 
 
+def _ddp_streams_steps_worker(rank, world, port, q, steps=3):
+    """Three optimizer steps under DDP with static_graph (bucket rebuild after the first iteration, the
+    side-stream AccumulateGrad nodes reused): every step's all-reduced gradients, towers on two streams
+    and on one."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "mamba-clip_amd"))
+        from types import SimpleNamespace
+        import torch.distributed as dist
+        from mamba_clip_amd.loss import ClipLoss
+        from mamba_clip_amd.model import build_clip
+        from mamba_clip_amd.train import wrap_ddp
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        args = SimpleNamespace(distributed=True, ddp_static_graph=True, ddp_bucket_mb=1)
+        res = {}
+        for conc in (True, False):
+            torch.manual_seed(0)
+            inner = build_clip("tiny-mamba-clip").to(dev)
+            inner.concurrent_towers = conc
+            model = wrap_ddp(inner, args, dev)
+            opt = torch.optim.SGD(inner.parameters(), lr=0.05)
+            grads, joined = [], []
+            for step in range(steps):
+                g = torch.Generator().manual_seed(100 * step + 5 + rank)
+                images = torch.randn(8, 3, 32, 32, generator=g).to(dev)
+                texts = torch.randint(1, 999, (8, 16), generator=g).to(dev)
+                opt.zero_grad(set_to_none=True)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = model(images, texts)
+                    loss = ClipLoss(rank=rank, world_size=world)(**out)["contrastive_loss"]
+                loss.backward()
+                torch.cuda.synchronize()
+                grads.append(torch.cat([p.grad.float().flatten() for p in inner.parameters()]).cpu().numpy())
+                joined.append(bool(inner.ddp_streams_joined))
+                opt.step()
+            torch.cuda.synchronize()
+            res[conc] = (grads, joined)
+        q.put((rank, {"conc": res[True][0], "seq": res[False][0], "joined": res[True][1]}))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+@pytest.mark.gpu
+def test_ddp_two_stream_towers_three_steps_static_graph_gloo_gpu_w2():
+    """the two-stream DDP path over 3 optimizer steps with static_graph (DDP rebuilds
+    its buckets after the first iteration and reuses the side-stream AccumulateGrad nodes): every step's
+    all-reduced gradients bitwise equal to the one-stream run, and equal on both ranks."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_streams_steps_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert all(out[r]["joined"])
+        assert len(out[r]["conc"]) == 3
+        for step, (gc, gs) in enumerate(zip(out[r]["conc"], out[r]["seq"])):
+            np.testing.assert_array_equal(gc, gs, err_msg=f"rank {r} step {step}")
+    for step in range(3):
+        np.testing.assert_array_equal(out[0]["conc"][step], out[1]["conc"][step])
+
+
 @pytest.mark.gpu
 def test_ddp_two_stream_towers_gloo_gpu_w2():
     """wrap_ddp with ClipModel's text tower on a second stream (comm hook joining the streams before
