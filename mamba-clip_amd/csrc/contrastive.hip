@@ -828,13 +828,20 @@ __global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, in
       const uint4 b1 = *reinterpret_cast<const uint4*>(sb + (((c0 + 1) ^ sw) << 4));
       return i32x8{(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
     };
-    i32x8 bf = bfrag(0);
+    // two fragment buffers: step ks + 1's LDS reads are issued before step ks's MFMAs (sched_barrier keeps
+    // the scheduler from sinking them behind the MFMAs, where they would wait for the operand read)
+    i32x8 bfa = bfrag(0), bfb = bfa;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const i32x8 bcur = bf;
-      if (ks + 1 < NKS) bf = bfrag(ks + 1);   // next fragment's LDS reads under this step's MFMAs
+      if (ks + 1 < NKS) {
+        if (ks & 1) bfa = bfrag(ks + 1);
+        else bfb = bfrag(ks + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const i32x8 bcur = (ks & 1) ? bfb : bfa;
       acc0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bcur, af[0][ks], acc0, 0, 0, 0, 127, 0, 127);
       acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bcur, af[1][ks], acc1, 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- epilogue: C^T fragments -> this wave's LDS block [64 rows][32 cols] (row m = l & 31 of block rb,
     // columns 8 i + 4 (l >> 5) + [0, 4))

@@ -251,6 +251,16 @@ __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
 #ifdef MC_SCALAR_PK
   return pmul(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x});
 #endif
+#ifdef MC_BCAST_C
+  return a * f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x};
+#endif
+#ifdef MC_SEL1_SCALAR
+  if constexpr (kHi) {
+    float x, y;
+    asm("v_mul_f32 %0, %2, %4\n\tv_mul_f32 %1, %3, %4" : "=&v"(x), "=&v"(y) : "v"(a.x), "v"(a.y), "v"(s.y));
+    return f32x2{x, y};
+  }
+#endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
   else asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
@@ -261,6 +271,17 @@ template <int kHi>
 __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
 #ifdef MC_SCALAR_PK
   return pfma(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x}, c);
+#endif
+#ifdef MC_BCAST_C
+  return a * f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x} + c;
+#endif
+#ifdef MC_SEL1_SCALAR
+  if constexpr (kHi) {
+    float x, y;
+    asm("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6" : "=&v"(x), "=&v"(y)
+        : "v"(a.x), "v"(a.y), "v"(s.y), "v"(c.x), "v"(c.y));
+    return f32x2{x, y};
+  }
 #endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
