@@ -484,10 +484,10 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
         for (int t = 0; t < kQT; ++t) {
 #pragma unroll
           for (int p = 0; p < kQP; ++p) {
-            const f32x2 arg = (t & 1) ? pk_mul_bcast<1>(A2[p], sc.dt[t >> 1]) : pk_mul_bcast<0>(A2[p], sc.dt[t >> 1]);
+            const f32x2 arg = (t & 1) ? pk_mul_bcast_safe<1>(A2[p], sc.dt[t >> 1]) : pk_mul_bcast_safe<0>(A2[p], sc.dt[t >> 1]);
             const f32x2 aa = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
             const f32x2 bb = bpair(kQT * s + t, p);
-            const f32x2 bu = (t & 1) ? pk_mul_bcast<1>(bb, sc.dtu[t >> 1]) : pk_mul_bcast<0>(bb, sc.dtu[t >> 1]);
+            const f32x2 bu = (t & 1) ? pk_mul_bcast_safe<1>(bb, sc.dtu[t >> 1]) : pk_mul_bcast_safe<0>(bb, sc.dtu[t >> 1]);
             x[p] = aa * x[p] + bu;
           }
         }
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
         f32x2 as[kQT], xs[kQT];
 #pragma unroll
         for (int t = 0; t < kQT; ++t) {
-          const f32x2 arg = (t & 1) ? pk_mul_bcast<1>(a2p, sc.dt[t >> 1]) : pk_mul_bcast<0>(a2p, sc.dt[t >> 1]);
+          const f32x2 arg = (t & 1) ? pk_mul_bcast_safe<1>(a2p, sc.dt[t >> 1]) : pk_mul_bcast_safe<0>(a2p, sc.dt[t >> 1]);
           as[t] = f32x2{pexp2(arg.x), pexp2(arg.y)};
         }
         {   // (B dt u off the chain: one pk_fma per step on it)
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
 #pragma unroll
           for (int t = 0; t < kQT; ++t) {
             const f32x2 bb = bpair(kQT * s + t, p);
-            const f32x2 bu = (t & 1) ? pk_mul_bcast<1>(bb, sc.dtu[t >> 1]) : pk_mul_bcast<0>(bb, sc.dtu[t >> 1]);
+            const f32x2 bu = (t & 1) ? pk_mul_bcast_safe<1>(bb, sc.dtu[t >> 1]) : pk_mul_bcast_safe<0>(bb, sc.dtu[t >> 1]);
             x = pfma(as[t], x, bu);
             xs[t] = x;
           }
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
           f32x2 red[kQT];
 #pragma unroll
           for (int t = 0; t < kQT; ++t)
-            red[t] = (t & 1) ? pk_mul_bcast<1>(xs[t], sc.gy[t >> 1]) : pk_mul_bcast<0>(xs[t], sc.gy[t >> 1]);
+            red[t] = (t & 1) ? pk_mul_bcast_safe<1>(xs[t], sc.gy[t >> 1]) : pk_mul_bcast_safe<0>(xs[t], sc.gy[t >> 1]);
           const float v = pair_reduce16(red, lane);
           if ((lane & 2) == 0)
             dbc[((kQT * s + (lane >> 3)) * 2 + 1) * kQN + 8 * h + 2 * p + ((lane >> 2) & 1)] = v;
@@ -569,15 +569,15 @@ __global__ __launch_bounds__(64 * kQW, 2) void scan_bwd_pair_kernel(const BwdPai
           for (int t = kQT - 1; t >= 0; --t) {
             const f32x4 q = qn;
             if (t > 0) qn = bquad(kQT * s + t - 1, p);
-            lam = (t & 1) ? pk_fma_bcast<1>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha)
-                          : pk_fma_bcast<0>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha);
+            lam = (t & 1) ? pk_fma_bcast_safe<1>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha)
+                          : pk_fma_bcast_safe<0>(q.hi, sc.gy[t >> 1], t == kQT - 1 ? hcar[p] : ha);
             if (hasZ) Y2[t] = pfma(q.hi, xs[t], Y2[t]);
             S2[t] = pfma(lam, q.lo, S2[t]);
-            red[t] = (t & 1) ? pk_mul_bcast<1>(lam, sc.dtu[t >> 1]) : pk_mul_bcast<0>(lam, sc.dtu[t >> 1]);
+            red[t] = (t & 1) ? pk_mul_bcast_safe<1>(lam, sc.dtu[t >> 1]) : pk_mul_bcast_safe<0>(lam, sc.dtu[t >> 1]);
             ha = pmul(lam, as[t]);
             const f32x2 hax = pmul(ha, t > 0 ? xs[t - 1] : xin);
             Q2[t] = pfma(hax, a2p, Q2[t]);
-            dap = (t & 1) ? pk_fma_bcast<1>(hax, sc.dt[t >> 1], dap) : pk_fma_bcast<0>(hax, sc.dt[t >> 1], dap);
+            dap = (t & 1) ? pk_fma_bcast_safe<1>(hax, sc.dt[t >> 1], dap) : pk_fma_bcast_safe<0>(hax, sc.dt[t >> 1], dap);
           }
           asm volatile("" : "+v"(ha), "+v"(dap));
 #pragma unroll

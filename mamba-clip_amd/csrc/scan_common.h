@@ -288,6 +288,32 @@ __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
   else asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
   return r;
 }
+// The same products without the op_sel[src] = 1 form (the LOW result reading a source's HIGH half):
+// gfx950 returned wrong low-half results for lanes 48-63 of v_pk_mul_f32 / v_pk_fma_f32 in that form
+// while another kernel ran on the CU (run-to-run differences of the two-stream training step, DESIGN
+// 4.9; the compiler never emits the form for packed fp32).  kHi = 1 is two scalar ops reading s.hi
+// directly; kHi = 0 keeps the packed op (op_sel_hi only: the HIGH result reads s.lo).
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_mul_bcast_safe(f32x2 a, f32x2 s) {
+  if constexpr (kHi) {
+    float x, y;
+    asm("v_mul_f32 %0, %2, %4\n\tv_mul_f32 %1, %3, %4" : "=&v"(x), "=&v"(y) : "v"(a.x), "v"(a.y), "v"(s.y));
+    return f32x2{x, y};
+  } else {
+    return pk_mul_bcast<0>(a, s);
+  }
+}
+template <int kHi>
+__device__ __forceinline__ f32x2 pk_fma_bcast_safe(f32x2 a, f32x2 s, f32x2 c) {
+  if constexpr (kHi) {
+    float x, y;
+    asm("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6" : "=&v"(x), "=&v"(y)
+        : "v"(a.x), "v"(a.y), "v"(s.y), "v"(c.x), "v"(c.y));
+    return f32x2{x, y};
+  } else {
+    return pk_fma_bcast<0>(a, s, c);
+  }
+}
 // exp2 of two values on the packed-FMA pipe (no transcendental): round-to-nearest split x = j + f
 // with the 1.5 * 2^23 shifter, a degree-6 near-minimax polynomial for 2^f on [-0.5, 0.5] (relative
 // error 9.6e-8), j added into the exponent field.  For x in [-126, 126].  A/B lever for the forward

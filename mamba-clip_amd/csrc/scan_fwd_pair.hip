@@ -289,18 +289,18 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
 #pragma unroll
           for (int p = 0; p < kPH / 2; ++p) {
             // dt broadcast from its half of the {dt, dt} register pair
-            const f32x2 arg = (e & 1) ? pk_mul_bcast<1>(A2[p], e < 2 ? q0.xy : q1.xy)
-                                      : pk_mul_bcast<0>(A2[p], e < 2 ? q0.xy : q1.xy);
+            const f32x2 arg = (e & 1) ? pk_mul_bcast_safe<1>(A2[p], e < 2 ? q0.xy : q1.xy)
+                                      : pk_mul_bcast_safe<0>(A2[p], e < 2 ? q0.xy : q1.xy);
             if (p < MC_FWD_POLY_PAIRS) dA[p] = exp2_poly2(arg);   // A/B lever (default 0: all v_exp_f32)
             else dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
           }
           {   // du broadcast from its half of {du, du}
             const f32x2 dup = e < 2 ? q0.zw : q1.zw;
             if (e & 1) {
-              x[0] = pk_fma_bcast<1>(b0.lo, dup, dA[0] * x[0]);
-              x[1] = pk_fma_bcast<1>(b0.hi, dup, dA[1] * x[1]);
-              x[2] = pk_fma_bcast<1>(b1.lo, dup, dA[2] * x[2]);
-              x[3] = pk_fma_bcast<1>(b1.hi, dup, dA[3] * x[3]);
+              x[0] = pk_fma_bcast_safe<1>(b0.lo, dup, dA[0] * x[0]);
+              x[1] = pk_fma_bcast_safe<1>(b0.hi, dup, dA[1] * x[1]);
+              x[2] = pk_fma_bcast_safe<1>(b1.lo, dup, dA[2] * x[2]);
+              x[3] = pk_fma_bcast_safe<1>(b1.hi, dup, dA[3] * x[3]);
             } else {
               x[0] = pk_fma_bcast<0>(b0.lo, dup, dA[0] * x[0]);
               x[1] = pk_fma_bcast<0>(b0.hi, dup, dA[1] * x[1]);

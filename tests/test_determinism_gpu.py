@@ -2,10 +2,12 @@
 
 * One stream (ClipModel.concurrent_towers False): the C2 model (real widths, batch 32) trained for three
   AdamW steps twice in one process ends with bitwise-equal parameters.
-* Two streams on ONE hardware queue (GPU_MAX_HW_QUEUES=1, set before HIP starts, so a subprocess): the
-  same, with the towers concurrent -- the configuration measured reproducible in every run
-  (profiles/r05/determinism/); with several hardware queues the Mamba tower's scan-backward gradients
-  still vary from run to run in some timings.
+* Two streams, the default (several hardware queues) and ONE hardware queue (GPU_MAX_HW_QUEUES=1, set
+  before HIP starts, so a subprocess): the same, with the towers concurrent.  Until round 6 the default
+  case was not reproducible: the scan backward's inline-asm packed-fp32 broadcast (v_pk_fma_f32 /
+  v_pk_mul_f32 whose low result reads a source's high half) gave wrong low halves in lanes 48-63 now and
+  then while a kernel of the other tower ran beside it; that form is gone from the scan kernels
+  (scan_common.h pk_*_bcast_safe, DESIGN 4.9, profiles/r06/determinism/).
 * The reductions that replaced torch's in the towers' glue (mc_colsum, mc_l2norm) give the same bits
   beside concurrent library GEMMs as on an idle device (torch's cross-workgroup batch sum did not:
   ~0.1 % of its outputs were wrong, tools/sum_under_load.py)."""
@@ -74,6 +76,12 @@ def _run(concurrent, batch, hw_queues=None):
 def test_one_stream_three_steps_bitwise_reproducible():
     same, moved, two = _run(concurrent=False, batch=32)
     assert moved and not two
+    assert same
+
+
+def test_two_streams_default_hw_queues_three_steps_bitwise_reproducible():
+    same, moved, two = _run(concurrent=True, batch=32)
+    assert moved and two, "the towers did not run on two streams"
     assert same
 
 

@@ -47,13 +47,11 @@ def test_graphed_step_matches_eager(model_name, batch):
 
 def test_two_stream_graphed_step_tracks_eager():
     """The towers' two-stream fork / join captured as two graph branches (GraphedStep(concurrent=True))
-    replays and tracks the eager two-stream step.  Not to the one-stream capture's 1e-3: at this batch the
-    eager two-stream step itself is not run-to-run reproducible with several hardware queues (two eager
-    runs measured 1.4654 vs 1.4669 at step 4: the Mamba tower's scan-backward parameter gradients, DESIGN
-    4.9), so the replays are held to 1e-2 relative on the loss and 2e-2 (+ AdamW's 2 lr per step) on the
-    parameters.  (With one
-    hardware queue, where the eager step is reproducible, capturing the two branches ended the process
-    with SIGSEGV inside the runtime: not used.)"""
+    replays and tracks the eager two-stream step to the same bounds as the one-stream capture (1e-3
+    relative on the loss, bf16-level on the parameters: hipBLASLt may pick other solutions under
+    capture, so not bitwise).  Since the scan kernels lost the packed op_sel broadcast form (DESIGN
+    4.9) the eager two-stream step is itself bitwise reproducible, and two captures of the same step
+    replay to the same bits (below)."""
     from mamba_clip_amd.train import GraphedStep, train_step
     m0, o0, l0, a0, (img, txt, tgt) = _setup("vit_b16-mamba130m", 8, 11)
     m0.concurrent_towers = True
@@ -67,9 +65,25 @@ def test_two_stream_graphed_step_tracks_eager():
     assert m1.concurrent_towers
     graphed = [float(step()["loss"].detach()) for _ in range(3)]
     for e, g in zip(eager[3:], graphed):
-        assert abs(e - g) <= 1e-2 * abs(e) + 1e-4, (eager, graphed)
-    # AdamW moves every element by up to lr per step whatever its gradient's size, so a near-zero
-    # gradient that differs in sign moves an element 2 lr apart (the zero-initialised biases): the
-    # parameters are held to 2e-2 of their scale plus 2 lr per step
+        assert abs(e - g) <= 1e-3 * abs(e) + 1e-4, (eager, graphed)
     for (n, p0), p1 in zip(m0.named_parameters(), m1.parameters()):
-        assert float((p0 - p1).abs().max()) <= 2e-2 * float(p0.abs().max()) + 2 * a0.lr * 6, n
+        assert float((p0 - p1).abs().max()) <= 1e-2 * float(p0.abs().max()) + 1e-6, n
+
+
+def test_two_stream_graph_replays_bitwise_reproducible():
+    """Two captures of the two-stream step from the same initial state replay three steps to bitwise
+    equal losses and parameters."""
+    from mamba_clip_amd.train import GraphedStep
+    runs = []
+    for _ in range(2):
+        m, o, l, a, (img, txt, tgt) = _setup("vit_b16-mamba130m", 8, 11)
+        m.concurrent_towers = True
+        step = GraphedStep(m, img, txt, tgt, l, o, a, warmup=3, concurrent=True)
+        losses = [step()["loss"].detach().clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((losses, [p.detach().clone() for p in m.parameters()]))
+        del step, m, o
+        torch.cuda.empty_cache()
+    (la, pa), (lb, pb) = runs
+    assert all(torch.equal(x, y) for x, y in zip(la, lb)), (la, lb)
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
