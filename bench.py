@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="pairs per GPU")
     ap.add_argument("--model", default="vit_b16-mamba130m")
     ap.add_argument("--scan-iters", type=int, default=20)
+    ap.add_argument("--graph-streams", type=int, default=2, choices=(1, 2),
+                    help="with --graph 1: capture the towers on two streams (2) or one (1)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay the step as one HIP graph (train.GraphedStep; single process), 0: eager, "
                          "-1: graph when world size is 1 and inputs are resident (default 0 until measured)")
@@ -345,7 +347,9 @@ def main():
             return train_step(model, *next(feed), loss, optimizer, None, targs)
     elif use_graph:
         from mamba_clip_amd.train import GraphedStep
-        step = GraphedStep(model, images, texts, targets, loss, optimizer, targs)
+        # the towers' two streams are captured as two graph branches (reproducible since round 6)
+        step = GraphedStep(model, images, texts, targets, loss, optimizer, targs,
+                           concurrent=bool(getattr(inner, "concurrent_towers", False)) and args.graph_streams == 2)
     else:
         def step():
             return train_step(model, images, texts, targets, loss, optimizer, None, targs)
@@ -397,7 +401,7 @@ def main():
         "config": {"workload": workload,
                    "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                    "seq_len": seq_len, "image_size": 224, "input": args.input,
-                   "step_launch": "hip-graph replay" if use_graph else "eager",
+                   "step_launch": (f"hip-graph replay ({args.graph_streams} streams)" if use_graph else "eager"),
                    "parallelism": f"dp{world}",
                    "library_gemm_selection": "tunableop-file" if gemm_tuned else "default-heuristic"},
         "mfma_estimate": {"flop_per_pair": flop_pair,

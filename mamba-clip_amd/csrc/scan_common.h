@@ -289,10 +289,16 @@ __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
   return r;
 }
 // The same products without the op_sel[src] = 1 form (the LOW result reading a source's HIGH half):
-// gfx950 returned wrong low-half results for lanes 48-63 of v_pk_mul_f32 / v_pk_fma_f32 in that form
-// while another kernel ran on the CU (run-to-run differences of the two-stream training step, DESIGN
-// 4.9; the compiler never emits the form for packed fp32).  kHi = 1 is two scalar ops reading s.hi
-// directly; kHi = 0 keeps the packed op (op_sel_hi only: the HIGH result reads s.lo).
+// in that form, issued from our inline asm, gfx950 returned wrong low-half results for lanes 48-63 of
+// v_pk_mul_f32 / v_pk_fma_f32 now and then while another kernel ran beside it (run-to-run differences of
+// the two-stream training step).  kHi = 1 is two scalar ops reading s.hi directly; kHi = 0
+// keeps the packed op (op_sel_hi only: the HIGH result reads s.lo).  Where one s.hi feeds several
+// products, hi_to_lo() moves it to a low half once and the packed kHi = 0 form broadcasts it.
+__device__ __forceinline__ f32x2 hi_to_lo(f32x2 s) {   // {s.hi, unspecified}: one v_mov, no op_sel
+  f32x2 r = __builtin_nondeterministic_value(r);
+  r.x = s.y;
+  return r;
+}
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_mul_bcast_safe(f32x2 a, f32x2 s) {
   if constexpr (kHi) {

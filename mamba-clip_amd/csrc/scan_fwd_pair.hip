@@ -286,28 +286,20 @@ __global__ __launch_bounds__(64, kMinW) void scan_fwd_pair_kernel(const FwdArgs 
           }
           __builtin_amdgcn_sched_barrier(0);   // keep the reads a step ahead (the scheduler sinks them to their use)
           f32x2 dA[kPH / 2];
+          // dt / du of position e: the low half of their register pairs (odd e: moved there once,
+          // scan_common.h hi_to_lo), broadcast by the packed ops
+          const f32x2 dtp = (e & 1) ? hi_to_lo(e < 2 ? q0.xy : q1.xy) : (e < 2 ? q0.xy : q1.xy);
+          const f32x2 dup = (e & 1) ? hi_to_lo(e < 2 ? q0.zw : q1.zw) : (e < 2 ? q0.zw : q1.zw);
 #pragma unroll
           for (int p = 0; p < kPH / 2; ++p) {
-            // dt broadcast from its half of the {dt, dt} register pair
-            const f32x2 arg = (e & 1) ? pk_mul_bcast_safe<1>(A2[p], e < 2 ? q0.xy : q1.xy)
-                                      : pk_mul_bcast_safe<0>(A2[p], e < 2 ? q0.xy : q1.xy);
+            const f32x2 arg = pk_mul_bcast<0>(A2[p], dtp);
             if (p < MC_FWD_POLY_PAIRS) dA[p] = exp2_poly2(arg);   // A/B lever (default 0: all v_exp_f32)
             else dA[p] = f32x2{fast_exp2(arg.x), fast_exp2(arg.y)};
           }
-          {   // du broadcast from its half of {du, du}
-            const f32x2 dup = e < 2 ? q0.zw : q1.zw;
-            if (e & 1) {
-              x[0] = pk_fma_bcast_safe<1>(b0.lo, dup, dA[0] * x[0]);
-              x[1] = pk_fma_bcast_safe<1>(b0.hi, dup, dA[1] * x[1]);
-              x[2] = pk_fma_bcast_safe<1>(b1.lo, dup, dA[2] * x[2]);
-              x[3] = pk_fma_bcast_safe<1>(b1.hi, dup, dA[3] * x[3]);
-            } else {
-              x[0] = pk_fma_bcast<0>(b0.lo, dup, dA[0] * x[0]);
-              x[1] = pk_fma_bcast<0>(b0.hi, dup, dA[1] * x[1]);
-              x[2] = pk_fma_bcast<0>(b1.lo, dup, dA[2] * x[2]);
-              x[3] = pk_fma_bcast<0>(b1.hi, dup, dA[3] * x[3]);
-            }
-          }
+          x[0] = pk_fma_bcast<0>(b0.lo, dup, dA[0] * x[0]);
+          x[1] = pk_fma_bcast<0>(b0.hi, dup, dA[1] * x[1]);
+          x[2] = pk_fma_bcast<0>(b1.lo, dup, dA[2] * x[2]);
+          x[3] = pk_fma_bcast<0>(b1.hi, dup, dA[3] * x[3]);
           f32x2 y2 = c0v.lo * x[0];
           y2 = c0v.hi * x[1] + y2;
           y2 = c1v.lo * x[2] + y2;
