@@ -45,8 +45,14 @@ def test_l2_normalize_matches_torch(rows, cols, dtype):
     xr = x.double().requires_grad_(True)
     yr = torch.nn.functional.normalize(xr, dim=-1)
     yr.backward(gy.double())
-    assert y.dtype == torch.float32
-    assert torch.allclose(y.double(), yr, atol=1e-6, rtol=1e-5)
+    # torch's dtype rule: the input's dtype outside autocast, fp32 under it (ops.l2_normalize)
+    assert y.dtype == dtype
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya = ops.l2_normalize(x)
+    assert ya.dtype == torch.float32
+    assert torch.allclose(ya.double(), yr, atol=1e-6, rtol=1e-5)
+    ytol = 1e-5 if dtype == torch.float32 else (4e-3 if dtype == torch.bfloat16 else 5e-4)
+    assert torch.allclose(y.double(), yr, atol=ytol, rtol=ytol)
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     scale = float(xr.grad.abs().max()) + 1e-30
     assert float((xa.grad.double() - xr.grad).abs().max()) / scale < tol
