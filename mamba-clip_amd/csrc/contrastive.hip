@@ -728,7 +728,7 @@ constexpr int kP8MaxTiles = 32;              // tiles per workgroup (column fact
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <typename TOut, int NKS>
-__global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, int nr, int tpr) {
+__global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, int nr, int tpr, int ilv) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kP8Stage + 8 * kP8EpWave * 4 + kP8MaxTiles * kP8Cols * 4];
   float* ep_all = reinterpret_cast<float*>(lds + 2 * kP8Stage);
   float* colf = ep_all + 8 * kP8EpWave;        // alpha * column factor of the workgroup's columns
@@ -738,8 +738,12 @@ __global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, in
   const int nrange = lin / g.tiles_m, panel = lin % g.tiles_m;
   const int m0 = panel * kP8Rows;
   const int ntiles = (g.N + kP8Cols - 1) / kP8Cols;
-  const int t0 = nrange * tpr, t1 = min(ntiles, t0 + tpr);
-  if (t0 >= t1) return;   // uniform across the workgroup
+  // the workgroup's B tiles: j = 0 .. cnt - 1 -> tile_of(j); contiguous (t0 + j) or, with ilv, every nr-th
+  // (nrange + j nr: the n-ranges of one panel then write neighbouring 256-B row pieces at the same time)
+  const int t0 = ilv ? nrange : nrange * tpr;
+  const int cnt = ilv ? max(0, (ntiles - nrange + nr - 1) / nr) : max(0, min(ntiles, t0 + tpr) - t0);
+  const int tstep = ilv ? nr : 1;
+  if (cnt <= 0) return;   // uniform across the workgroup
   const uint8_t* __restrict__ A = reinterpret_cast<const uint8_t*>(g.A);
   const uint8_t* __restrict__ B = reinterpret_cast<const uint8_t*>(g.B);
   constexpr int kChunks = 4 * NKS;             // 16-B chunks of a row (K = 64 NKS bytes)
@@ -770,9 +774,9 @@ __global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, in
   }
   {
     const float alpha = g.alpha_dev ? *g.alpha_dev : g.alpha;
-    const int ncols = (t1 - t0) * kP8Cols;
+    const int ncols = cnt * kP8Cols;
     for (int i = tid; i < ncols; i += 512) {
-      const int n = t0 * kP8Cols + i;
+      const int n = (t0 + (i / kP8Cols) * tstep) * kP8Cols + i % kP8Cols;
       colf[i] = alpha * ((g.sb && n < g.N) ? g.sb[n] : 1.f);
     }
   }
@@ -808,15 +812,16 @@ __global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, in
   const int nl = cg * 32 + (lane & 31);        // this lane's B row (tile column) in the fragment reads
 
   issue(t0, 0);
-  for (int t = t0; t < t1; ++t) {
-    const int st = (t - t0) & 1;
+  for (int j = 0; j < cnt; ++j) {
+    const int t = t0 + j * tstep;
+    const int st = j & 1;
     // this wave's DMA of tile t landed (the previous tile's kStores stores may stay in flight), this
     // wave's LDS reads of tile t - 1 are done, then everyone's: stage st is readable, st ^ 1 is free
-    if (t == t0) __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+    if (j == 0) __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
     else if constexpr (kStores == 8) __builtin_amdgcn_s_waitcnt(0x0078);   // vmcnt(8) lgkmcnt(0)
     else __builtin_amdgcn_s_waitcnt(0x0074);                                // vmcnt(4) lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
-    if (t + 1 < t1) issue(t + 1, st ^ 1);
+    if (j + 1 < cnt) issue(t + tstep, st ^ 1);
     asm volatile("" ::: "memory");
 
     const char* sb = lds + st * kP8Stage + nl * kP8Row;
@@ -855,7 +860,7 @@ __global__ __launch_bounds__(512, 1) void sim8_panel_kernel(const GemmArgs g, in
     }
     asm volatile("" ::: "memory");   // one wave's LDS operations run in program order
     const int n_w = t * kP8Cols + cg * 32 + ec;                       // first output column of this lane
-    const float* cf = colf + (t - t0) * kP8Cols + cg * 32 + ec;
+    const float* cf = colf + j * kP8Cols + cg * 32 + ec;
     const bool col_ok = n_w < g.N;                                    // N % 8 == 0: whole vectors
 #pragma unroll
     for (int j = 0; j < kStores; ++j) {
@@ -1138,8 +1143,17 @@ void launch_sim8_panel_t(const GemmArgs& g0, hipStream_t s) {
   const int tpr = (ntiles + nr - 1) / nr;
   nr = (ntiles + tpr - 1) / tpr;               // no empty n-ranges
   const dim3 grid(g.tiles_m * nr), block(512);
+  // interleaved n-ranges for fp32 logits (C5: 87 -> 70 us, the 8 n-ranges of a panel write one 2-KB row
+  // piece per tile step instead of eight 256-B pieces 4 KB apart); bf16 logits keep contiguous ranges
+  // (51.6 vs 60 us in a launch loop, equal under graph replay: profiles/r06/c5/interleave_ab.txt).
+  // MAMBA_CLIP_AMD_SIM8_INTERLEAVE=0 / 1 forces either (A/B).
+  static const int env_ilv = [] {
+    const char* e = getenv("MAMBA_CLIP_AMD_SIM8_INTERLEAVE");
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  const int ilv = env_ilv >= 0 ? env_ilv : (sizeof(TOut) == 4 ? 1 : 0);
   switch (g.K / 64) {
-#define MC_P8(NK) case NK: hipLaunchKernelGGL((sim8_panel_kernel<TOut, NK>), grid, block, 0, s, g, nr, tpr); break;
+#define MC_P8(NK) case NK: hipLaunchKernelGGL((sim8_panel_kernel<TOut, NK>), grid, block, 0, s, g, nr, tpr, ilv); break;
     MC_P8(1) MC_P8(2) MC_P8(3) MC_P8(4) MC_P8(5) MC_P8(6) MC_P8(7) MC_P8(8)
 #undef MC_P8
     default: break;
