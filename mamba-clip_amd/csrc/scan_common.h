@@ -244,44 +244,41 @@ __device__ __forceinline__ float pexp2(float a) {
 #else
 __device__ __forceinline__ float pexp2(float a) { return fast_exp2(a); }
 #endif
-// a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1): one v_pk_mul_f32 with op_sel
-// (the compiler otherwise moves an odd-register scalar to an even register first)
+// MC_DIAG_OPSEL_HI (diagnostic build only) restores the round-5 form of the high-half broadcasts (the
+// packed op_sel:[0,1] ops below) so that the determinism A/B variants can be rebuilt; the
+// product build rejects that form at compile time.
+#ifdef MC_DIAG_OPSEL_HI
+constexpr bool kDiagOpselHi = true;
+#else
+constexpr bool kDiagOpselHi = false;
+#endif
+// a * {s.lo, s.lo} (kHi = 0) or a * {s.hi, s.hi} (kHi = 1, diagnostic only): one v_pk_mul_f32 with
+// op_sel (the compiler otherwise moves an odd-register scalar to an even register first)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 s) {
+  static_assert(kHi == 0 || kDiagOpselHi, "the op_sel high-half broadcast is diagnostic only (DESIGN 4.9): "
+                                          "use pk_mul_bcast_safe");
 #ifdef MC_SCALAR_PK
   return pmul(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x});
 #endif
 #ifdef MC_BCAST_C
   return a * f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x};
 #endif
-#ifdef MC_SEL1_SCALAR
-  if constexpr (kHi) {
-    float x, y;
-    asm("v_mul_f32 %0, %2, %4\n\tv_mul_f32 %1, %3, %4" : "=&v"(x), "=&v"(y) : "v"(a.x), "v"(a.y), "v"(s.y));
-    return f32x2{x, y};
-  }
-#endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
   else asm(MC_ASM_HEAD "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s));
   return r;
 }
-// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason)
+// a * s.{lo|hi} + c: one v_pk_fma_f32 with op_sel (same reason; kHi = 1 diagnostic only)
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 s, f32x2 c) {
+  static_assert(kHi == 0 || kDiagOpselHi, "the op_sel high-half broadcast is diagnostic only (DESIGN 4.9): "
+                                          "use pk_fma_bcast_safe");
 #ifdef MC_SCALAR_PK
   return pfma(a, f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x}, c);
 #endif
 #ifdef MC_BCAST_C
   return a * f32x2{kHi ? s.y : s.x, kHi ? s.y : s.x} + c;
-#endif
-#ifdef MC_SEL1_SCALAR
-  if constexpr (kHi) {
-    float x, y;
-    asm("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6" : "=&v"(x), "=&v"(y)
-        : "v"(a.x), "v"(a.y), "v"(s.y), "v"(c.x), "v"(c.y));
-    return f32x2{x, y};
-  }
 #endif
   f32x2 r;
   if constexpr (kHi) asm(MC_ASM_HEAD "v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" MC_ASM_TAIL : "=v"(r) : "v"(a), "v"(s), "v"(c));
@@ -301,7 +298,9 @@ __device__ __forceinline__ f32x2 hi_to_lo(f32x2 s) {   // {s.hi, unspecified}: o
 }
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_mul_bcast_safe(f32x2 a, f32x2 s) {
-  if constexpr (kHi) {
+  if constexpr (kHi && kDiagOpselHi) {
+    return pk_mul_bcast<1>(a, s);
+  } else if constexpr (kHi) {
     float x, y;
     asm("v_mul_f32 %0, %2, %4\n\tv_mul_f32 %1, %3, %4" : "=&v"(x), "=&v"(y) : "v"(a.x), "v"(a.y), "v"(s.y));
     return f32x2{x, y};
@@ -311,7 +310,9 @@ __device__ __forceinline__ f32x2 pk_mul_bcast_safe(f32x2 a, f32x2 s) {
 }
 template <int kHi>
 __device__ __forceinline__ f32x2 pk_fma_bcast_safe(f32x2 a, f32x2 s, f32x2 c) {
-  if constexpr (kHi) {
+  if constexpr (kHi && kDiagOpselHi) {
+    return pk_fma_bcast<1>(a, s, c);
+  } else if constexpr (kHi) {
     float x, y;
     asm("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6" : "=&v"(x), "=&v"(y)
         : "v"(a.x), "v"(a.y), "v"(s.y), "v"(c.x), "v"(c.y));
