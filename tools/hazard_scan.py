@@ -120,8 +120,9 @@ def main(path, window=2):
         ln, mnem, dst, src, asm_c, text, kern = it
         if not mnem.startswith("v_"):
             continue
-        # gfx950 packed fp32 with op_sel[src] = 1 (the LOW result reading a source's HIGH half): wrong low
-        # halves in lanes 48-63 under concurrent load; the compiler never emits it
+        # gfx950 packed fp32 with op_sel[src] = 1 (the LOW result reading a source's HIGH half): from our
+        # inline asm it gave wrong low halves in lanes 48-63 under concurrent load; the
+        # compiler emits it too in a few places outside the scan kernels (conv1d_fwd, SS2D merge_bwd)
         m_os = re.search(r"op_sel:\[([01,]+)\]", text)
         if re.match(r"^v_pk_(fma|mul|add)_f32", mnem) and m_os and "1" in m_os.group(1):
             findings.append(("pk_f32 op_sel hi->lo", kern, ln, text, ln, text, asm_c, asm_c))
@@ -144,6 +145,10 @@ def main(path, window=2):
                     findings.append(("pk_f32->valu", kern, pln, ptext, ln, text, asm_p, asm_c))
                 if is_perm and ws < 2:
                     findings.append(("valu->permlane", kern, pln, ptext, ln, text, asm_p, asm_c))
+    return findings
+
+
+def report(findings):
     seen = {}
     for f in findings:
         kind, kern, pln, ptext, ln, text, asm_p, asm_c = f
@@ -159,4 +164,4 @@ def main(path, window=2):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    report(main(sys.argv[1]))
