@@ -451,11 +451,11 @@ class ClipModel(nn.Module):
     @property
     def side_tower(self):
         """Which tower runs on the side stream: the text tower, for every text tower.  Round 4 put the
-        image tower there beside the Mamba text tower (C2 -0.3 ms, profiles/r04/stream_priority/), but
-        that arrangement is not run-to-run reproducible: the Mamba tower's step-1 gradients differ from
-        run to run (10 distinct outcomes in 12, from the first scan backward on) while the text-on-side
-        arrangement repeats bitwise (profiles/r05/determinism/).  MAMBA_CLIP_AMD_SIDE_TOWER=
-        image restores it for A/B."""
+        image tower there beside the Mamba text tower (C2 -0.3 ms, profiles/r04/stream_priority/); in
+        round 5 that arrangement was not run-to-run reproducible (the scan backward's packed op_sel
+        broadcast, found and removed in round 6) and the two measured the same on one box
+        (3683 vs 3684 pairs/s), so the text tower stays on the side stream.  MAMBA_CLIP_AMD_SIDE_TOWER=
+        image restores the other arrangement for A/B."""
         env = os.environ.get("MAMBA_CLIP_AMD_SIDE_TOWER")
         if env in ("text", "image"):
             return env

@@ -277,10 +277,10 @@ class GraphedStep:
         autocast = self.autocast_for(args)
         inner = unwrap_model(model)
         # One stream by default: replay order = eager order, and the replays are bitwise repeatable.
-        # concurrent=True captures the towers' two-stream fork / join as two graph branches (round 5:
-        # with the glue reductions deterministic, DESIGN 4.9, the replays match the eager two-stream step
-        # to the tolerance below; tests/test_graph_gpu.py).  The flag is restored after the capture, so
-        # later eager steps run the towers concurrently again.
+        # concurrent=True captures the towers' two-stream fork / join as two graph branches; since the
+        # round-6 scan fix two captures replay to the same bits and track the eager
+        # two-stream step to the one-stream bounds (tests/test_graph_gpu.py).  The flag is restored after
+        # the capture, so later eager steps run the towers concurrently again.
         prev = getattr(inner, "concurrent_towers", False)
         if not concurrent:
             inner.concurrent_towers = False
