@@ -96,6 +96,33 @@ typedef struct mc_ss2d_merge_bwd_params {
 size_t mc_ss2d_merge_bwd_workspace_bytes(int32_t batch, int32_t height, int32_t width, int32_t channels);
 int mc_ss2d_merge_ln_gate_bwd(const mc_ss2d_merge_bwd_params* p, void* stream);
 
+/*
+ * mc_ss2d_group_proj: the per-direction projections of SS2D (model.py:519-528, x_proj and dt_proj as
+ * einsums over the four directions, in fp32: model.py:531-537) and their input gradients, as one
+ * grouped product over sequence slabs, without operand permutes:
+ *
+ *   Y[b][g][m][l] = (acc ? A[b][g][m][l] : 0) + sum_n W[g][m][n] * X[b][g % x_group_mod][n][l]
+ *
+ * for b < batch, g < groups, m < rows_out, n < rows_in, l < seqlen; fp32 everywhere; the sum over n
+ * runs in order (deterministic).  Element addresses (in floats): W at g*w_gs + m*w_ms + n*w_ns,
+ * X at b*x_bs + (g % x_group_mod)*x_gs + n*x_ns + l, A at b*a_bs + g*a_gs + m*a_ms + l, Y likewise with
+ * y_*.  A may alias Y (in-place accumulation).  Uses (SS2D, k = 2 i + j the direction):
+ *   x_dbl[b,k] = x_proj[k] u[b, k % 2]       (x_group_mod 2: u = [x, x^T] holds two frames)
+ *   delta[b,k] = dt_proj[k] x_dbl[b,k,:R]    (the dt rows)
+ *   d(dt rows)[b,k] = dt_proj[k]^T ddelta[b,k]   (w_ms / w_ns swapped)
+ *   du[b,j] = x_proj[j]^T dx_dbl[b,j] + x_proj[2+j]^T dx_dbl[b,2+j]   (two calls, the second with acc)
+ */
+typedef struct mc_ss2d_group_proj_params {
+  int32_t batch, groups, rows_out, rows_in, seqlen;
+  int32_t x_group_mod;      /* >= 1 */
+  const float* w;  int64_t w_gs, w_ms, w_ns;
+  const float* x;  int64_t x_bs, x_gs, x_ns;
+  const float* acc; int64_t a_bs, a_gs, a_ms;     /* nullable */
+  float* y;        int64_t y_bs, y_gs, y_ms;
+} mc_ss2d_group_proj_params;
+
+int mc_ss2d_group_proj(const mc_ss2d_group_proj_params* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

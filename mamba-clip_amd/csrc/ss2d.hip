@@ -735,3 +735,94 @@ extern "C" int mc_ss2d_merge_ln_gate_bwd(const mc_ss2d_merge_bwd_params* p, void
   if (p->dln_bias) reduce_partials(nwg, f.channels, a.ws + f.channels, 2 * (int64_t)f.channels, p->dln_bias, s);
   return check_launch("mc_ss2d_merge_ln_gate_bwd (partials)");
 }
+
+// ------------------------------------------------------------------ grouped projections (mc_ss2d_group_proj)
+// Y[b][g][m][l] = A + sum_n W[g][m][n] X[b][g % mod][n][l].  Lane = position (64 consecutive l: the
+// X[n][l] loads are coalesced 256-B rows); a wave owns kGpM output rows, so each X value feeds kGpM FMAs
+// from registers and W[g][m][n] is wave-uniform (scalar loads; with m contiguous, w_ms == 1, one
+// 64-B scalar load per n).  Long reductions (rows_in >= 64) split n over the workgroup's 4 waves,
+// whose partial sums meet in LDS and are added in wave order; short ones give each wave its own row
+// chunk.  Every sum runs in a fixed order: deterministic.
+constexpr int kGpM = 16;     // output rows per wave
+constexpr int kGpW = 4;      // waves per workgroup
+
+template <bool kSplitN, bool kMC>
+__global__ __launch_bounds__(64 * kGpW) void group_proj_kernel(const mc_ss2d_group_proj_params p) {
+  __shared__ float part[kSplitN ? (kGpW - 1) * kGpM * 64 : 1];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l = blockIdx.x * 64 + lane;
+  const int bg = blockIdx.y;
+  const int b = bg / p.groups, g = bg % p.groups;
+  const int m0 = (kSplitN ? blockIdx.z : blockIdx.z * kGpW + w) * kGpM;
+  if (!kSplitN && m0 >= p.rows_out) return;          // wave-uniform (no barrier in this form)
+  const int n0 = kSplitN ? (int)(((int64_t)w * p.rows_in) / kGpW) : 0;
+  const int n1 = kSplitN ? (int)(((int64_t)(w + 1) * p.rows_in) / kGpW) : p.rows_in;
+  const bool ok = l < p.seqlen;
+  const int lc = ok ? l : p.seqlen - 1;
+  const float* __restrict__ X = p.x + (int64_t)b * p.x_bs + (int64_t)(g % p.x_group_mod) * p.x_gs + lc;
+  const float* __restrict__ W = p.w + (int64_t)g * p.w_gs + (int64_t)m0 * (kMC ? 1 : p.w_ms);
+  const int mcount = min(kGpM, p.rows_out - m0);
+  auto wv = [&](int i, int n) __attribute__((always_inline)) {
+    return kMC ? W[(int64_t)n * p.w_ns + i] : W[(int64_t)i * p.w_ms + (int64_t)n * p.w_ns];
+  };
+  float acc[kGpM];
+#pragma unroll
+  for (int i = 0; i < kGpM; ++i) acc[i] = 0.f;
+  int n = n0;
+  for (; n + 4 <= n1; n += 4) {
+    float xv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xv[q] = X[(int64_t)(n + q) * p.x_ns];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n + q), xv[q], acc[i]);   // rows past M: never stored
+  }
+  for (; n < n1; ++n) {
+    const float xv = X[(int64_t)n * p.x_ns];
+#pragma unroll
+    for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n), xv, acc[i]);
+  }
+  if constexpr (kSplitN) {
+    if (w > 0) {
+#pragma unroll
+      for (int i = 0; i < kGpM; ++i) part[((w - 1) * kGpM + i) * 64 + lane] = acc[i];
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int v = 0; v < kGpW - 1; ++v)
+#pragma unroll
+      for (int i = 0; i < kGpM; ++i) acc[i] += part[(v * kGpM + i) * 64 + lane];
+  }
+  if (!ok) return;
+  const float* A = p.acc ? p.acc + (int64_t)b * p.a_bs + (int64_t)g * p.a_gs + (int64_t)m0 * p.a_ms + l : nullptr;
+  float* Y = p.y + (int64_t)b * p.y_bs + (int64_t)g * p.y_gs + (int64_t)m0 * p.y_ms + l;
+#pragma unroll
+  for (int i = 0; i < kGpM; ++i)
+    if (i < mcount) Y[(int64_t)i * p.y_ms] = (A ? A[(int64_t)i * p.a_ms] : 0.f) + acc[i];
+}
+
+extern "C" int mc_ss2d_group_proj(const mc_ss2d_group_proj_params* p, void* stream) {
+  MC_CHECK(p != nullptr, MC_ERR_INVALID, "mc_ss2d_group_proj: null params");
+  MC_CHECK(p->batch >= 0 && p->groups >= 1 && p->rows_out >= 0 && p->rows_in >= 0 && p->seqlen >= 0 &&
+               p->x_group_mod >= 1 && p->x_group_mod <= p->groups,
+           MC_ERR_SHAPE, "mc_ss2d_group_proj: bad shape (B %d G %d M %d N %d L %d mod %d)", p->batch, p->groups,
+           p->rows_out, p->rows_in, p->seqlen, p->x_group_mod);
+  MC_CHECK(p->rows_out <= 4096 && (int64_t)p->batch * p->groups < 65536, MC_ERR_SHAPE,
+           "mc_ss2d_group_proj: rows_out %d (<= 4096) or batch * groups %lld (< 65536) out of range", p->rows_out,
+           (long long)p->batch * p->groups);
+  MC_CHECK(p->w && p->y && (p->x || p->rows_in == 0), MC_ERR_INVALID, "mc_ss2d_group_proj: null pointer");
+  if ((int64_t)p->batch * p->rows_out * p->seqlen == 0) return MC_OK;
+  const bool split = p->rows_in >= 64;
+  const bool mc = p->w_ms == 1;
+  const dim3 grid((p->seqlen + 63) / 64, p->batch * p->groups,
+                  split ? (p->rows_out + kGpM - 1) / kGpM : (p->rows_out + kGpM * kGpW - 1) / (kGpM * kGpW));
+  hipStream_t s = (hipStream_t)stream;
+  if (split && mc) hipLaunchKernelGGL((group_proj_kernel<true, true>), grid, dim3(64 * kGpW), 0, s, *p);
+  else if (split) hipLaunchKernelGGL((group_proj_kernel<true, false>), grid, dim3(64 * kGpW), 0, s, *p);
+  else if (mc) hipLaunchKernelGGL((group_proj_kernel<false, true>), grid, dim3(64 * kGpW), 0, s, *p);
+  else hipLaunchKernelGGL((group_proj_kernel<false, false>), grid, dim3(64 * kGpW), 0, s, *p);
+  return check_launch("mc_ss2d_group_proj");
+}

@@ -192,6 +192,18 @@ class SS2DMergeParams(ctypes.Structure):
     ]
 
 
+class SS2DGroupProjParams(ctypes.Structure):
+    """Mirror of ``mc_ss2d_group_proj_params`` (include/mc_ss2d.h)."""
+    _fields_ = [
+        ("batch", c_i32), ("groups", c_i32), ("rows_out", c_i32), ("rows_in", c_i32), ("seqlen", c_i32),
+        ("x_group_mod", c_i32),
+        ("w", c_fp), ("w_gs", c_i64), ("w_ms", c_i64), ("w_ns", c_i64),
+        ("x", c_fp), ("x_bs", c_i64), ("x_gs", c_i64), ("x_ns", c_i64),
+        ("acc", c_fp), ("a_bs", c_i64), ("a_gs", c_i64), ("a_ms", c_i64),
+        ("y", c_fp), ("y_bs", c_i64), ("y_gs", c_i64), ("y_ms", c_i64),
+    ]
+
+
 class SS2DMergeBwdParams(ctypes.Structure):
     """Mirror of ``mc_ss2d_merge_bwd_params`` (include/mc_ss2d.h)."""
     _fields_ = [
@@ -312,6 +324,7 @@ SYMBOLS = {
     "mc_ss2d_merge_ln_gate_fwd": (ctypes.c_int, [ctypes.POINTER(SS2DMergeParams), c_vp]),
     "mc_ss2d_merge_ln_gate_bwd": (ctypes.c_int, [ctypes.POINTER(SS2DMergeBwdParams), c_vp]),
     "mc_ss2d_merge_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32]),
+    "mc_ss2d_group_proj": (ctypes.c_int, [ctypes.POINTER(SS2DGroupProjParams), c_vp]),
 }
 
 _lib = None

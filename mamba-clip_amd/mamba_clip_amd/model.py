@@ -35,7 +35,7 @@ from . import GEMM_GRIDS_DATA_PARALLEL
 from .ops import (GradHandoff, GradSlab, _compute_dtype, add_layernorm, add_pos, add_rmsnorm, attn_supported,
                   causal_conv1d, l2_normalize, linear_sk, mixer_proj, mixer_proj_ok, mlp, neg_exp_many,
                   packed_attention, patch_im2col, qkv_proj, split_rows, split_rows_n, ss2d_conv_stack,
-                  ss2d_merge_ln_gate, token_embed, weight_cast_scope, wleft_mm)
+                  ss2d_merge_ln_gate, ss2d_proj, ss2d_proj_ok, token_embed, weight_cast_scope, wleft_mm)
 from .selective_scan_interface import (SS2D_REVERSE_GROUPS, SS2D_U_GROUPS, ProjectedScanFn, SelectiveScanFn,
                                        fine_state_scope,
                                        grouped_scan_fn, projected_scan_ok, selective_scan_fn)
@@ -746,10 +746,14 @@ class SS2D(nn.Module):
         un-flipped.  Blocks 1 / 3 stay in the transposed (W, H) frame: the merge reads them there."""
         Bsz, _, d, L = u.shape
         K = 4
-        w = self.x_proj_weight.to(u.dtype).view(2, 2, -1, d)                # [i][j]: direction k = 2 i + j
-        x_dbl = torch.einsum("bjdl,ijcd->bijcl", u, w).reshape(Bsz, K, -1, L)
-        dts, Bs, Cs = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=2)
-        dts = torch.einsum("bkrl,kdr->bkdl", dts, self.dt_projs_weight.to(u.dtype))
+        wx, wdt = self.x_proj_weight.to(u.dtype), self.dt_projs_weight.to(u.dtype)
+        if ss2d_proj_ok(u, wx, wdt):
+            # both projections on mc_ss2d_group_proj, no permuted operand copies (ops.SS2DProjFn)
+            dts, Bs, Cs = ss2d_proj(u, wx, wdt, self.dt_rank, self.d_state)
+        else:
+            x_dbl = torch.einsum("bjdl,ijcd->bijcl", u, wx.view(2, 2, -1, d)).reshape(Bsz, K, -1, L)   # k = 2 i + j
+            dts, Bs, Cs = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=2)
+            dts = torch.einsum("bkrl,kdr->bkdl", dts, wdt)
         return grouped_scan_fn(u.float().reshape(Bsz, 2 * d, L), dts.float().reshape(Bsz, K * d, L),
                                -torch.exp(self.A_logs.float()), Bs.float(), Cs.float(), self.Ds.float(),
                                self.dt_projs_bias.float().reshape(-1), delta_softplus=True,

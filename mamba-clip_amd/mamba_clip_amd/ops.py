@@ -1727,6 +1727,98 @@ def ss2d_conv_stack(x, weight, bias):
     return SS2DConvStackFn.apply(x, weight, bias)
 
 
+def _group_proj(w, wstr, x, xstr, y, ystr, B, G, M, Nn, L, mod=None, acc=None, astr=None):
+    """One mc_ss2d_group_proj launch: Y[b,g,m,l] = A + sum_n W[g,m,n] X[b,g % mod,n,l] (fp32).
+    wstr = (g, m, n) strides of W; xstr = (b, g, n) of X; ystr / astr = (b, g, m) of Y / A."""
+    p = _lib.SS2DGroupProjParams()
+    p.batch, p.groups, p.rows_out, p.rows_in, p.seqlen = B, G, M, Nn, L
+    p.x_group_mod = mod or G
+    p.w, (p.w_gs, p.w_ms, p.w_ns) = w.data_ptr(), wstr
+    p.x, (p.x_bs, p.x_gs, p.x_ns) = x.data_ptr(), xstr
+    if acc is not None:
+        p.acc, (p.a_bs, p.a_gs, p.a_ms) = acc.data_ptr(), astr
+    p.y, (p.y_bs, p.y_gs, p.y_ms) = y.data_ptr(), ystr
+    _lib.check(_lib.load().mc_ss2d_group_proj(ctypes.byref(p), _lib.stream_handle(y.device)), "mc_ss2d_group_proj")
+
+
+def _wpad(t):
+    """t's values (contiguous, fp32) in a buffer with 16 floats of zero slack after them:
+    mc_ss2d_group_proj reads whole 16-row weight chunks and drops the rows past M."""
+    buf = torch.zeros(t.numel() + 16, device=t.device, dtype=torch.float32)
+    buf[:t.numel()].copy_(t.reshape(-1))
+    return buf
+
+
+def ss2d_proj_ok(u, w_x, w_dt):
+    """Shapes / dtypes SS2DProjFn takes: fp32 CUDA u (B, 2, d, L) contiguous, fp32 weights."""
+    return (u.is_cuda and u.dtype == torch.float32 and u.dim() == 4 and u.shape[1] == 2 and u.is_contiguous()
+            and w_x.dtype == torch.float32 and w_dt.dtype == torch.float32 and w_x.shape[0] == 4
+            and w_x.shape[2] == u.shape[2] and w_dt.shape[1] == u.shape[2] and u.shape[2] <= 4096)
+
+
+class SS2DProjFn(torch.autograd.Function):
+    """SS2D's per-direction projections (reference model.py:519-528, in fp32 as model.py:531-537): with
+    u = [x, x^T] (B, 2, d, L) holding the two frames and direction k = 2 i + j reading frame j,
+        x_dbl[b,k] = x_proj[k] u[b, j]      (c = R + 2N rows: dt, B, C)
+        delta[b,k] = dt_proj[k] x_dbl[b,k,:R]
+    on mc_ss2d_group_proj -- no permuted operand copies (torch.einsum made ~10 elementwise copies and
+    tiny-K library GEMMs around them).  Backward: d(dt rows) and du on the same kernel (du as
+    two in-order passes over i), the weight gradients as batched GEMMs over L summed over the batch in a
+    fixed order (ops.colsum).  Returns (delta, B rows, C rows) as (B, 4, ., L) views / tensors."""
+
+    @staticmethod
+    def forward(ctx, u, w_x, w_dt, R, N):
+        Bsz, _, d, L = u.shape
+        c = R + 2 * N
+        wx, wdt = w_x.contiguous(), w_dt.contiguous()
+        x_dbl = torch.empty(Bsz, 4, c, L, device=u.device, dtype=torch.float32)
+        delta = torch.empty(Bsz, 4, d, L, device=u.device, dtype=torch.float32)
+        # weights with the output row contiguous (one 64-B scalar load per n and 16 rows): [k][n][m]
+        wx_t = _wpad(wx.transpose(1, 2))
+        wdt_t = _wpad(wdt.transpose(1, 2))
+        _group_proj(wx_t, (c * d, 1, c), u, (2 * d * L, d * L, L), x_dbl, (4 * c * L, c * L, L), Bsz, 4, c, d, L, mod=2)
+        _group_proj(wdt_t, (d * R, 1, d), x_dbl, (4 * c * L, c * L, L), delta, (4 * d * L, d * L, L), Bsz, 4, d, R, L)
+        ctx.save_for_backward(u, wx, wdt, x_dbl)
+        ctx.rn = (R, N)
+        return delta, x_dbl[:, :, R:R + N], x_dbl[:, :, R + N:]
+
+    @staticmethod
+    def backward(ctx, g_delta, g_B, g_C):
+        u, wx, wdt, x_dbl = ctx.saved_tensors
+        R, N = ctx.rn
+        Bsz, _, d, L = u.shape
+        c = R + 2 * N
+        dx = torch.empty(Bsz, 4, c, L, device=u.device, dtype=torch.float32)
+        wx_p, wdt_p = _wpad(wx), _wpad(wdt)   # [k][c][d] / [k][d][R]: already output-row contiguous here
+        if g_delta is None:
+            dx[:, :, :R].zero_()
+            g_delta = torch.zeros(Bsz, 4, d, L, device=u.device, dtype=torch.float32)
+        else:
+            g_delta = g_delta.float().contiguous()
+            # d(dt rows)[b,k] = dt_proj[k]^T ddelta[b,k]
+            _group_proj(wdt_p, (d * R, 1, R), g_delta, (4 * d * L, d * L, L), dx, (4 * c * L, c * L, L), Bsz, 4, R, d, L)
+        for off, g in ((R, g_B), (R + N, g_C)):
+            if g is None:
+                dx[:, :, off:off + N].zero_()
+            else:
+                dx[:, :, off:off + N].copy_(g)
+        # du[b,j] = x_proj[j]^T dx[b,j] + x_proj[2+j]^T dx[b,2+j]: two passes, the second accumulating in place
+        du = torch.empty_like(u)
+        _group_proj(wx_p, (c * d, 1, d), dx, (4 * c * L, c * L, L), du, (2 * d * L, d * L, L), Bsz, 2, d, c, L)
+        _group_proj(wx_p[2 * c * d:], (c * d, 1, d), dx[:, 2:], (4 * c * L, c * L, L), du, (2 * d * L, d * L, L), Bsz, 2,
+                    d, c, L, acc=du, astr=(2 * d * L, d * L, L))
+        # weight gradients: per-batch GEMMs over L, summed over the batch in a fixed order
+        dwx = torch.stack([torch.matmul(dx[:, 2 * i:2 * i + 2], u.transpose(-1, -2)) for i in range(2)], dim=1)
+        dwx = colsum(dwx.reshape(Bsz, 4 * c * d)).view(4, c, d)
+        dwdt = torch.matmul(g_delta, x_dbl[:, :, :R].transpose(-1, -2))          # (B, 4, d, R)
+        dwdt = colsum(dwdt.reshape(Bsz, 4 * d * R)).view(4, d, R)
+        return du, dwx, dwdt, None, None
+
+
+def ss2d_proj(u, w_x, w_dt, R, N):
+    return SS2DProjFn.apply(u, w_x, w_dt, R, N)
+
+
 class SS2DMergeFn(torch.autograd.Function):
     """y = LayerNorm(((y1 + y2) + y3) + y4) * silu(z), channels-last, from the grouped scan's
     (B, 4C, H*W) fp32 output (directions 1 / 3 in the x^T frame) -- reference model.py:553-565 flips /

@@ -114,3 +114,70 @@ def test_ss2d_kernels_reject_bad_shapes():
     x = torch.randn(1, 4, 4, 8, device=DEV)
     with pytest.raises(RuntimeError, match="ksize"):
         ss2d_conv_stack(x, torch.randn(8, 1, 5, 5, device=DEV), None)
+
+
+PROJ_SHAPES = [(2, 64, 2, 3136), (2, 128, 4, 784), (3, 256, 8, 196), (2, 512, 16, 49), (1, 48, 3, 37),
+               (2, 16, 1, 5)]   # (B, d_inner, dt_rank, L): the medmamba stages + ragged / tiny cases
+
+
+@pytest.mark.parametrize("shape", PROJ_SHAPES)
+def test_ss2d_proj_matches_reference_einsums(shape):
+    """ops.SS2DProjFn (mc_ss2d_group_proj) vs the reference's two einsums (model.py:519-528) in fp64 on
+    the same fp32 inputs: x_dbl's B / C rows, delta, and the gradients of u, x_proj and dt_proj; and two
+    runs give the same bits (in-order sums, fixed-order batch reduction)."""
+    from mamba_clip_amd.ops import ss2d_proj
+    Bsz, d, R, L = shape
+    N = 16
+    c = R + 2 * N
+    g = torch.Generator().manual_seed(d + L)
+    u = torch.randn(Bsz, 2, d, L, generator=g)
+    wx = torch.randn(4, c, d, generator=g) * d ** -0.5
+    wdt = torch.randn(4, d, R, generator=g) * R ** -0.5
+    gd, gb, gc = (torch.randn(Bsz, 4, m, L, generator=g) for m in (d, N, N))
+    # reference: the model's einsum form in fp64 (direction k = 2 i + j reads frame j)
+    ur, wxr, wdtr = (t.double().requires_grad_(True) for t in (u, wx, wdt))
+    x_dbl = torch.einsum("bjdl,ijcd->bijcl", ur, wxr.view(2, 2, c, d)).reshape(Bsz, 4, c, L)
+    dts, Br, Cr = torch.split(x_dbl, [R, N, N], dim=2)
+    dr = torch.einsum("bkrl,kdr->bkdl", dts, wdtr)
+    torch.autograd.backward([dr, Br, Cr], [gd.double(), gb.double(), gc.double()])
+    runs = []
+    for _ in range(2):
+        ug, wxg, wdtg = (t.to(DEV).requires_grad_(True) for t in (u, wx, wdt))
+        delta, Bs, Cs = ss2d_proj(ug, wxg, wdtg, R, N)
+        torch.autograd.backward([delta, Bs, Cs], [gd.to(DEV), gb.to(DEV), gc.to(DEV)])
+        runs.append([t.detach().clone() for t in (delta, Bs, Cs, ug.grad, wxg.grad, wdtg.grad)])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    for got, ref, tol in zip(runs[0], (dr, Br, Cr, ur.grad, wxr.grad, wdtr.grad), (1e-5, 1e-5, 1e-5, 1e-5, 2e-5, 2e-5)):
+        assert got.shape == ref.shape
+        assert _rel(got.cpu(), ref.detach()) < tol
+
+
+def test_ss2d_block_uses_group_proj():
+    """The SS2D block's forward takes the mc_ss2d_group_proj path for fp32 activations, and its result
+    equals the einsum path's within fp32 rounding (fwd + every parameter gradient)."""
+    import mamba_clip_amd.model as M
+    torch.manual_seed(3)
+    m = M.SS2D(d_model=32).to(DEV)
+    x = torch.randn(2, 14, 14, 32, device=DEV)
+    calls = []
+    real = M.ss2d_proj
+    M.ss2d_proj = lambda *a: calls.append(1) or real(*a)
+    try:
+        xa = x.clone().requires_grad_(True)
+        m(xa).square().sum().backward()
+    finally:
+        M.ss2d_proj = real
+    assert calls, "SS2D did not take the group-projection path"
+    grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    ok = M.ss2d_proj_ok
+    M.ss2d_proj_ok = lambda *a: False
+    try:
+        xb = x.clone().requires_grad_(True)
+        m(xb).square().sum().backward()
+    finally:
+        M.ss2d_proj_ok = ok
+    assert _rel(xa.grad, xb.grad) < 1e-4
+    for n, p in m.named_parameters():
+        assert _rel(grads[n], p.grad) < 1e-4, n
