@@ -17,6 +17,8 @@
 //                   gradients in their own frames (the grouped scan backward reads them as dout).
 // One thread owns one pixel and 4 consecutive channels (16-B fp32 / 8-B 16-bit channels-last
 // vectors, 8 threads cover a 32-channel block).
+#include <type_traits>
+
 #include "mc_common.h"
 #include "../../include/mc_ss2d.h"
 
@@ -763,27 +765,34 @@ __global__ __launch_bounds__(64 * kGpW) void group_proj_kernel(const mc_ss2d_gro
   const float* __restrict__ X = p.x + (int64_t)b * p.x_bs + (int64_t)(g % p.x_group_mod) * p.x_gs + lc;
   const float* __restrict__ W = p.w + (int64_t)g * p.w_gs + (int64_t)m0 * (kMC ? 1 : p.w_ms);
   const int mcount = min(kGpM, p.rows_out - m0);
-  auto wv = [&](int i, int n) __attribute__((always_inline)) {
-    return kMC ? W[(int64_t)n * p.w_ns + i] : W[(int64_t)i * p.w_ms + (int64_t)n * p.w_ns];
-  };
   float acc[kGpM];
 #pragma unroll
   for (int i = 0; i < kGpM; ++i) acc[i] = 0.f;
-  int n = n0;
-  for (; n + 4 <= n1; n += 4) {
-    float xv[4];
+  // a whole 16-row chunk reads 16 consecutive weights per n (one scalar load when m is contiguous); the
+  // last, partial chunk re-reads its last row for the rows past M (computed, never stored)
+  auto sweep = [&](auto full) __attribute__((always_inline)) {
+    auto wv = [&](int i, int n) __attribute__((always_inline)) {
+      const int ie = decltype(full)::value ? i : min(i, mcount - 1);
+      return kMC ? W[(int64_t)n * p.w_ns + ie] : W[(int64_t)ie * p.w_ms + (int64_t)n * p.w_ns];
+    };
+    int n = n0;
+    for (; n + 4 <= n1; n += 4) {
+      float xv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xv[q] = X[(int64_t)(n + q) * p.x_ns];
+      for (int q = 0; q < 4; ++q) xv[q] = X[(int64_t)(n + q) * p.x_ns];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n + q), xv[q], acc[i]);   // rows past M: never stored
-  }
-  for (; n < n1; ++n) {
-    const float xv = X[(int64_t)n * p.x_ns];
+        for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n + q), xv[q], acc[i]);
+    }
+    for (; n < n1; ++n) {
+      const float xv = X[(int64_t)n * p.x_ns];
 #pragma unroll
-    for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n), xv, acc[i]);
-  }
+      for (int i = 0; i < kGpM; ++i) acc[i] = fmaf(wv(i, n), xv, acc[i]);
+    }
+  };
+  if (mcount == kGpM) sweep(std::true_type());
+  else sweep(std::false_type());
   if constexpr (kSplitN) {
     if (w > 0) {
 #pragma unroll

@@ -1741,14 +1741,6 @@ def _group_proj(w, wstr, x, xstr, y, ystr, B, G, M, Nn, L, mod=None, acc=None, a
     _lib.check(_lib.load().mc_ss2d_group_proj(ctypes.byref(p), _lib.stream_handle(y.device)), "mc_ss2d_group_proj")
 
 
-def _wpad(t):
-    """t's values (contiguous, fp32) in a buffer with 16 floats of zero slack after them:
-    mc_ss2d_group_proj reads whole 16-row weight chunks and drops the rows past M."""
-    buf = torch.zeros(t.numel() + 16, device=t.device, dtype=torch.float32)
-    buf[:t.numel()].copy_(t.reshape(-1))
-    return buf
-
-
 def ss2d_proj_ok(u, w_x, w_dt):
     """Shapes / dtypes SS2DProjFn takes: fp32 CUDA u (B, 2, d, L) contiguous, fp32 weights."""
     return (u.is_cuda and u.dtype == torch.float32 and u.dim() == 4 and u.shape[1] == 2 and u.is_contiguous()
@@ -1774,8 +1766,8 @@ class SS2DProjFn(torch.autograd.Function):
         x_dbl = torch.empty(Bsz, 4, c, L, device=u.device, dtype=torch.float32)
         delta = torch.empty(Bsz, 4, d, L, device=u.device, dtype=torch.float32)
         # weights with the output row contiguous (one 64-B scalar load per n and 16 rows): [k][n][m]
-        wx_t = _wpad(wx.transpose(1, 2))
-        wdt_t = _wpad(wdt.transpose(1, 2))
+        wx_t = wx.transpose(1, 2).contiguous()
+        wdt_t = wdt.transpose(1, 2).contiguous()
         _group_proj(wx_t, (c * d, 1, c), u, (2 * d * L, d * L, L), x_dbl, (4 * c * L, c * L, L), Bsz, 4, c, d, L, mod=2)
         _group_proj(wdt_t, (d * R, 1, d), x_dbl, (4 * c * L, c * L, L), delta, (4 * d * L, d * L, L), Bsz, 4, d, R, L)
         ctx.save_for_backward(u, wx, wdt, x_dbl)
@@ -1789,7 +1781,7 @@ class SS2DProjFn(torch.autograd.Function):
         Bsz, _, d, L = u.shape
         c = R + 2 * N
         dx = torch.empty(Bsz, 4, c, L, device=u.device, dtype=torch.float32)
-        wx_p, wdt_p = _wpad(wx), _wpad(wdt)   # [k][c][d] / [k][d][R]: already output-row contiguous here
+        wx_p, wdt_p = wx, wdt   # [k][c][d] / [k][d][R]: already output-row contiguous here
         if g_delta is None:
             dx[:, :, :R].zero_()
             g_delta = torch.zeros(Bsz, 4, d, L, device=u.device, dtype=torch.float32)
@@ -1805,10 +1797,10 @@ class SS2DProjFn(torch.autograd.Function):
         # du[b,j] = x_proj[j]^T dx[b,j] + x_proj[2+j]^T dx[b,2+j]: two passes, the second accumulating in place
         du = torch.empty_like(u)
         _group_proj(wx_p, (c * d, 1, d), dx, (4 * c * L, c * L, L), du, (2 * d * L, d * L, L), Bsz, 2, d, c, L)
-        _group_proj(wx_p[2 * c * d:], (c * d, 1, d), dx[:, 2:], (4 * c * L, c * L, L), du, (2 * d * L, d * L, L), Bsz, 2,
+        _group_proj(wx_p[2:], (c * d, 1, d), dx[:, 2:], (4 * c * L, c * L, L), du, (2 * d * L, d * L, L), Bsz, 2,
                     d, c, L, acc=du, astr=(2 * d * L, d * L, L))
         # weight gradients: per-batch GEMMs over L, summed over the batch in a fixed order
-        dwx = torch.stack([torch.matmul(dx[:, 2 * i:2 * i + 2], u.transpose(-1, -2)) for i in range(2)], dim=1)
+        dwx = torch.matmul(dx.view(Bsz, 2, 2, c, L), u.transpose(-1, -2).unsqueeze(1))   # [b][i][j] (k = 2 i + j)
         dwx = colsum(dwx.reshape(Bsz, 4 * c * d)).view(4, c, d)
         dwdt = torch.matmul(g_delta, x_dbl[:, :, :R].transpose(-1, -2))          # (B, 4, d, R)
         dwdt = colsum(dwdt.reshape(Bsz, 4 * d * R)).view(4, d, R)
