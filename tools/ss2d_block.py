@@ -40,6 +40,8 @@ def run(m, x, ops, iters):
         M.ss2d_conv_stack, M.ss2d_merge_ln_gate = FUSED
 
 
+if os.environ.get("SS2D_PROJ") == "0":          # A/B: the einsum projections instead of mc_ss2d_group_proj
+    M.ss2d_proj_ok = lambda *a: False
 torch.manual_seed(0)
 if "--trace" in sys.argv:
     m = M.SS2D(d_model=32).cuda()
